@@ -1,0 +1,200 @@
+/*
+ * co_env.h -- C ABI of the MI355X (gfx950) batched CO-environment engine.
+ *
+ * Drop-in boundary for the rl4co-slap hot path: the per-step env functions of
+ * TSP / CVRP / SLAP, the episode-end rewards + validity checks, the fused
+ * decode step and utils.ops.gather_by_index.  Each entry point replaces the
+ * ATen op sequence the reference issues at the cited file:line of
+ * j4n1k/rl4co-slap (reference @ 2025-02-02).
+ *
+ * Conventions (all entry points):
+ *  - plain device pointers + sizes; no torch / HIP types in the signatures;
+ *    `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *  - every call is stream-ordered and asynchronous: no allocation, no host
+ *    synchronisation, graph-capturable; the library never owns user memory;
+ *  - the caller allocates every output; outputs may alias their matching input
+ *    only where a parameter comment says so ("in-place allowed");
+ *  - return 0 on success, CO_E_* (< 0) for invalid arguments, or the positive
+ *    hipError_t of a failed launch.  Nothing throws across the ABI;
+ *  - data-dependent failures (invalid tour, capacity overflow, infeasible or
+ *    out-of-range index) are OR-ed into a caller-provided device word
+ *    `status` (bits CO_ST_*); the host maps them to the reference's
+ *    AssertionError / IndexError messages;
+ *  - dtypes are the reference TensorDict dtypes: bool/uint8 masks as bytes,
+ *    int64 indices, float32 coordinates/demands/rewards, int32 assignment.
+ */
+#ifndef CO_ENV_H
+#define CO_ENV_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CO_OK 0
+#define CO_E_INVAL (-1)     /* bad size / null pointer */
+#define CO_E_ALIGN (-2)     /* pointer misaligned for its dtype */
+#define CO_E_MODE (-3)      /* unknown mode */
+
+/* status bits (device int32, OR-ed atomically) */
+#define CO_ST_INVALID_TOUR 1      /* "Invalid tour"              tsp/env.py:173, cvrp/env.py:175 */
+#define CO_ST_OVER_CAPACITY 2     /* "Used more than capacity"   cvrp/env.py:188-190 */
+#define CO_ST_INFEASIBLE 4        /* "infeasible action selected" decoding.py:376-379 */
+#define CO_ST_INDEX_RANGE 8       /* index out of range (torch raises IndexError/RuntimeError) */
+
+/* Library identification: returns the gfx target string compiled in. */
+const char* co_build_info(void);
+
+/* ------------------------------------------------------------------ TSP */
+
+/* TSPEnv._reset (rl4co/envs/routing/tsp/env.py:95-120):
+ * action_mask[B,N] = 1, first_node[B] = current_node[B] = 0, i[B,1] = 0,
+ * reward[B,1] = 0.  first_node and current_node may be the same buffer
+ * (the reference aliases them). */
+int co_tsp_reset(int64_t batch, int64_t num_loc, uint8_t* action_mask, int64_t* first_node,
+                 int64_t* current_node, int64_t* i, float* reward, void* stream);
+
+/* TSPEnv._step (tsp/env.py:67-93):
+ *   first_out = (first_mode says the batch has an i == 0) ? action : first_in
+ *   mask_out  = mask_in with mask_out[b, action[b]] = 0       (in-place allowed)
+ *   done[b]   = sum(mask_out[b]) == 0 ; reward[b] = 0 (bool)
+ *   i_out     = i_in + 1 (in-place allowed); current_out = action (may be NULL)
+ * first_mode: 0 = keep first_in, 1 = take action, 2 = read *first_flag (device
+ * int32, nonzero = take action; produced by co_any_eq_i64).  This is the
+ * batch-wide `td["i"].all() == 0` test of tsp/env.py:70. */
+int co_tsp_step(int64_t batch, int64_t num_loc, const int64_t* action, const uint8_t* mask_in,
+                uint8_t* mask_out, const int64_t* i_in, int64_t* i_out, const int64_t* first_in,
+                int64_t* first_out, int64_t* current_out, uint8_t* done, uint8_t* reward,
+                int first_mode, const int32_t* first_flag, int32_t* status, void* stream);
+
+/* TSPEnv.get_reward (envs/common/base.py:182-188 + tsp/env.py:157-173):
+ * reward[b] = -closed tour length of locs[b, actions[b, 0..T-1]].
+ * actions element (b, t) lives at actions[b*act_stride_b + t*act_stride_t].
+ * check != 0: a row that is not a permutation of 0..T-1 sets CO_ST_INVALID_TOUR
+ * (the reference's sort(1) == arange(T) test). */
+int co_tsp_reward(int64_t batch, int64_t num_loc, int64_t steps, const float* locs,
+                  const int64_t* actions, int64_t act_stride_b, int64_t act_stride_t, int check,
+                  float* reward, int32_t* status, void* stream);
+
+/* ----------------------------------------------------------------- CVRP */
+
+/* CVRPEnv._reset + get_action_mask (cvrp/env.py:107-149).  N = customers.
+ * locs_out[B,N+1,2] = cat(depot[B,2], locs_in[B,N,2]); current_node[B,1] = 0;
+ * used_capacity[B,1] = 0; vehicle_capacity_out[B,1] = vehicle_capacity;
+ * visited[B,N+1] = 0; action_mask[B,N+1] per get_action_mask. */
+int co_cvrp_reset(int64_t batch, int64_t num_loc, const float* depot, const float* locs_in,
+                  const float* demand, float vehicle_capacity, float* locs_out,
+                  int64_t* current_node, float* used_capacity, float* vehicle_capacity_out,
+                  uint8_t* visited, uint8_t* action_mask, void* stream);
+
+/* CVRPEnv._step fused with get_action_mask (cvrp/env.py:73-105,137-149):
+ *   d = demand[b, clamp(a-1, 0, N-1)]; used_out = (used_in + d) * (a != 0)
+ *   visited_out = visited_in with [a] = 1 (in-place allowed); current_out = a
+ *   done = sum(visited_out) == N+1 ; reward = 0 (bool); action_mask recomputed. */
+int co_cvrp_step(int64_t batch, int64_t num_loc, const int64_t* action, const float* demand,
+                 const float* used_in, float* used_out, const float* vehicle_capacity,
+                 const uint8_t* visited_in, uint8_t* visited_out, int64_t* current_out,
+                 uint8_t* done, uint8_t* reward, uint8_t* action_mask, int32_t* status,
+                 void* stream);
+
+/* CVRPEnv.get_action_mask alone (cvrp/env.py:137-149). current_node is [B,1]. */
+int co_cvrp_action_mask(int64_t batch, int64_t num_loc, const float* demand, const float* used,
+                        const float* vehicle_capacity, const uint8_t* visited,
+                        const int64_t* current_node, uint8_t* action_mask, void* stream);
+
+/* CVRPEnv.get_reward (cvrp/env.py:151-190): reward = -tour length of
+ * [depot] + locs[actions] (closed).  check != 0 also runs
+ * check_solution_validity: customers 1..N exactly once, every other entry 0
+ * (CO_ST_INVALID_TOUR), then the per-step capacity scan
+ * used = max(used + d, 0) <= vehicle_capacity + 1e-5 (CO_ST_OVER_CAPACITY). */
+int co_cvrp_reward(int64_t batch, int64_t num_loc, int64_t steps, const float* locs,
+                   const int64_t* actions, int64_t act_stride_b, int64_t act_stride_t,
+                   const float* demand, const float* vehicle_capacity, int check, float* reward,
+                   int32_t* status, void* stream);
+
+/* ----------------------------------------------------------------- SLAP */
+
+/* SLAPEnv._reset (rl4co/envs/warehousing/slap/env.py:95-129). L = n_aisles*n_locs,
+ * P = products: action_mask[B,L] = 1 except column 0 (depot); to_choose[B,P] =
+ * 0..P-1 (float); i[B,1] = 0; reward[B,1] = 0; ratio[B,L] = 0 (ratio may be NULL). */
+int co_slap_reset(int64_t batch, int64_t num_slots, int64_t n_products, uint8_t* action_mask,
+                  float* to_choose, int64_t* i, float* reward, float* ratio, void* stream);
+
+/* SLAPEnv._step (slap/env.py:38-93): product p = (int)to_choose[b*tc_stride];
+ * assign_out = assign_in with [b, p] = (int)action[b] (in-place allowed:
+ * then only that element is written); mask_out = mask_in with [b, action] = 0
+ * (in-place allowed); done[b] = (i_in[b] == P-1); reward[b] = 0 (bool);
+ * i_out = i_in + 1.  Negative indices wrap like torch advanced indexing. */
+int co_slap_step(int64_t batch, int64_t num_slots, int64_t n_products, const int64_t* action,
+                 const float* to_choose, int64_t tc_stride, const int32_t* assign_in,
+                 int32_t* assign_out, const uint8_t* mask_in, uint8_t* mask_out,
+                 const int64_t* i_in, int64_t* i_out, uint8_t* done, uint8_t* reward,
+                 int32_t* status, void* stream);
+
+/* SLAPEnv._get_reward (slap/env.py:131-143): for each order o (in order),
+ * total -= closed Euclidean tour over locs[assignment[picklist[b, o, :]]]. */
+int co_slap_reward(int64_t batch, int64_t num_slots, int64_t n_products, int64_t n_orders,
+                   int64_t order_size, const int32_t* assignment, const int64_t* picklist,
+                   const float* locs, float* reward, int32_t* status, void* stream);
+
+/* ------------------------------------------------------------ utilities */
+
+/* utils.ops.gather_by_index (rl4co/utils/ops.py:65-77), gather along one dim:
+ * src element (o, j, :) at src + o*src_stride_outer + j*src_stride_len (bytes),
+ * `inner_bytes` contiguous bytes each; idx (o, m) at idx[o*idx_stride_outer +
+ * m*idx_stride_len]; dst[o, m, :] contiguous [outer, idx_len, inner_bytes].
+ * Out-of-range index: CO_ST_INDEX_RANGE and a zero-filled output element. */
+int co_gather_by_index(const void* src, int64_t outer, int64_t src_len, int64_t inner_bytes,
+                       int64_t src_stride_outer, int64_t src_stride_len, const int64_t* idx,
+                       int64_t idx_len, int64_t idx_stride_outer, int64_t idx_stride_len,
+                       void* dst, int32_t* status, void* stream);
+
+/* The batch-wide test of tsp/env.py:70: *flag = any(x[0..n) == value). */
+int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t* flag, void* stream);
+
+/* ---------------------------------------------------------- decode step */
+
+#define CO_DECODE_GREEDY 0
+#define CO_DECODE_SAMPLING 1
+#define CO_DECODE_EVALUATE 2
+
+/* DecodingStrategy.step (rl4co/utils/decoding.py:141-191,327-399,489-499):
+ * x = logits[b*logits_stride + c]; tanh clip (tanh_clipping > 0); masked
+ * (mask != NULL and mask[b*n+c] == 0) -> -inf; x /= temperature;
+ * logp = (x - max) - log(sum(exp(x - max)));
+ * greedy: first argmax of logp (torch tie-break); sampling: inverse CDF of
+ * exp(logp) with a Philox draw keyed by (seed, offset, b); evaluate: action_in.
+ * action_out[b], logp_sel[b] = logp[b, action]; logprobs_full (nullable)
+ * receives the whole row.  Greedy/sampling picking a masked action sets
+ * CO_ST_INFEASIBLE. */
+int co_decode_step(int64_t batch, int64_t n_actions, const float* logits, int64_t logits_stride,
+                   const uint8_t* mask, float tanh_clipping, float temperature, int mode,
+                   const int64_t* action_in, int64_t* action_out, float* logp_sel,
+                   float* logprobs_full, uint64_t seed, uint64_t offset, int32_t* status,
+                   void* stream);
+
+/* ------------------------------------------- bench policies (in-kernel) */
+
+/* Deterministic cheap policies for the env-throughput benchmark
+ * (SURVEY.md 8d); they are the "policy" half of a rollout, not reference code.
+ * TSP: step0 -> 0, then nearest unvisited to current_node (ties lowest index).
+ * CVRP: nearest feasible customer, else depot.  SLAP: free location with the
+ * lowest depot_loc_dist.  first_step != 0 selects the TSP step-0 branch. */
+int co_tsp_nearest_action(int64_t batch, int64_t num_loc, const float* locs,
+                          const uint8_t* action_mask, const int64_t* current_node, int first_step,
+                          int64_t* action_out, void* stream);
+int co_cvrp_nearest_action(int64_t batch, int64_t num_loc, const float* locs,
+                           const uint8_t* action_mask, const int64_t* current_node,
+                           int64_t* action_out, void* stream);
+int co_slap_closest_free_action(int64_t batch, int64_t num_slots, const float* depot_loc_dist,
+                                const uint8_t* action_mask, int64_t* action_out, void* stream);
+
+/* Number of rows with done[b] == 0 written to *count (device int32). */
+int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CO_ENV_H */

@@ -1,0 +1,113 @@
+"""ctypes binding of the gfx950 C-ABI library (``include/co_env.h``).
+
+The library is the product: every env/decode/gather call on a device tensor goes
+through it.  There is no CPU or PyTorch fallback -- if the library is missing or
+the tensors are not on a HIP device, calls raise.
+
+``torch`` is imported before the library is loaded so that ``libamdhip64.so.7``
+resolves (by SONAME) to the HIP runtime torch already mapped: one runtime per
+process, so torch streams and allocations are valid handles for the kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libco_env.so")
+
+_i64, _i32, _f32, _u64, _p = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
+
+# name -> argtypes (all return int status)
+_SIGS = {
+    "co_tsp_reset": [_i64, _i64, _p, _p, _p, _p, _p, _p],
+    "co_tsp_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p, _p],
+    "co_tsp_reward": [_i64, _i64, _i64, _p, _p, _i64, _i64, _i32, _p, _p, _p],
+    "co_cvrp_reset": [_i64, _i64, _p, _p, _p, _f32, _p, _p, _p, _p, _p, _p, _p],
+    "co_cvrp_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "co_cvrp_action_mask": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p],
+    "co_cvrp_reward": [_i64, _i64, _i64, _p, _p, _i64, _i64, _p, _p, _i32, _p, _p, _p],
+    "co_slap_reset": [_i64, _i64, _i64, _p, _p, _p, _p, _p, _p],
+    "co_slap_step": [_i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "co_slap_reward": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p],
+    "co_gather_by_index": [_p, _i64, _i64, _i64, _i64, _i64, _p, _i64, _i64, _i64, _p, _p, _p],
+    "co_any_eq_i64": [_p, _i64, _i64, _p, _p],
+    "co_decode_step": [_i64, _i64, _p, _i64, _p, _f32, _f32, _i32, _p, _p, _p, _p, _u64, _u64,
+                       _p, _p],
+    "co_tsp_nearest_action": [_i64, _i64, _p, _p, _p, _i32, _p, _p],
+    "co_cvrp_nearest_action": [_i64, _i64, _p, _p, _p, _p, _p],
+    "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],
+    "co_count_not_done": [_p, _i64, _p, _p],
+}
+
+ST_INVALID_TOUR = 1
+ST_OVER_CAPACITY = 2
+ST_INFEASIBLE = 4
+ST_INDEX_RANGE = 8
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+def load():
+    """Load (once) and return the ctypes handle; raise if the library is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                f"rl4co_slap_amd: HIP library {LIB_PATH} is missing; build it with "
+                "`python -m rl4co_slap_amd.csrc.build` (hipcc, gfx950). There is no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        lib.co_build_info.restype = ctypes.c_char_p
+        lib.co_build_info.argtypes = []
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return list(_SIGS) + ["co_build_info"]
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and t.device.type != "cuda":
+            raise RuntimeError(
+                "rl4co_slap_amd runs the env on the HIP device only (no CPU fallback); "
+                f"got a tensor on {t.device}. Move the TensorDict with td.to('cuda').")
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
+
+
+_status_cache = {}
+
+
+def scratch_status(device) -> torch.Tensor:
+    """A zeroed device int32 word for data-dependent error bits."""
+    return torch.zeros(1, dtype=torch.int32, device=device)

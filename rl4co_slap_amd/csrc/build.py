@@ -1,0 +1,58 @@
+"""Build the gfx950 C-ABI library ``rl4co_slap_amd/_lib/libco_env.so`` with hipcc.
+
+No torch types cross the ABI, so the library is a plain ``hipcc -shared`` build;
+it links ``libamdhip64.so.7`` by SONAME and therefore binds to the HIP runtime
+torch has already loaded when imported after ``import torch`` (one runtime per
+process).  Usage: ``python -m rl4co_slap_amd.csrc.build [--force]``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+OUT_DIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(OUT_DIR, "libco_env.so")
+SOURCES = ["tsp.hip", "cvrp.hip", "slap.hip", "ops.hip", "decode.hip"]
+HEADERS = ["co_common.hpp", "co_tile.hpp"]
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the gfx950 library cannot be built")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(HERE, f) for f in SOURCES + HEADERS]
+    deps.append(os.path.join(ROOT, "include", "co_env.h"))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    os.makedirs(OUT_DIR, exist_ok=True)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-result",
+           "-I", os.path.join(ROOT, "include"), "-o", tmp]
+    cmd += [os.path.join(HERE, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

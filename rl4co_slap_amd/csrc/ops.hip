@@ -1,0 +1,114 @@
+// utils.ops kernels for gfx950: gather_by_index (rl4co/utils/ops.py:65-77),
+// the batch-wide "any i == 0" test of tsp/env.py:70, the not-done counter used
+// by the rollout engine's done poll, and the build-info string.
+#include "co_common.hpp"
+
+using namespace co;
+
+namespace {
+
+// One thread per VW-byte unit of the output; the index of a unit's row is read
+// once per unit (L1/L2 hit for the 2nd..k-th unit of the same row).
+template <typename V>
+__global__ __launch_bounds__(256) void gather_kernel(const uint8_t* src, int64_t outer,
+                                                     int64_t src_len, int64_t units_per_elem,
+                                                     int64_t s_outer, int64_t s_len,
+                                                     const int64_t* idx, int64_t idx_len,
+                                                     int64_t i_outer, int64_t i_len, V* dst,
+                                                     int32_t* status) {
+  const int64_t total = outer * idx_len * units_per_elem;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total; u += stride) {
+    const int64_t e = u / units_per_elem;
+    const int64_t k = u - e * units_per_elem;
+    const int64_t o = e / idx_len;
+    const int64_t m = e - o * idx_len;
+    const int64_t j = idx[o * i_outer + m * i_len];
+    V v{};
+    if (j < 0 || j >= src_len) {
+      bad = true;
+    } else {
+      v = reinterpret_cast<const V*>(src + o * s_outer + j * s_len)[k];
+    }
+    dst[u] = v;
+  }
+  if (__any(bad) && lane_id() == 0) set_status(status, CO_ST_INDEX_RANGE);
+}
+
+__global__ __launch_bounds__(256) void any_eq_kernel(const int64_t* x, int64_t n, int64_t value,
+                                                     int32_t* flag) {
+  bool hit = false;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
+    hit |= x[k] == value;
+  if (__any(hit) && lane_id() == 0) atomicOr(flag, 1);
+}
+
+__global__ __launch_bounds__(256) void count_not_done_kernel(const uint8_t* done, int64_t n,
+                                                             int32_t* count) {
+  int c = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
+    c += done[k] == 0;
+  c = wave_sum(c);
+  if (lane_id() == 0 && c) atomicAdd(count, c);
+}
+
+}  // namespace
+
+extern "C" const char* co_build_info(void) {
+  return "rl4co_slap_amd co_env: gfx950 (CDNA4), wave64";
+}
+
+extern "C" int co_gather_by_index(const void* src, int64_t outer, int64_t src_len,
+                                  int64_t inner_bytes, int64_t s_outer, int64_t s_len,
+                                  const int64_t* idx, int64_t idx_len, int64_t i_outer,
+                                  int64_t i_len, void* dst, int32_t* status, void* stream) {
+  if (outer < 0 || src_len < 0 || idx_len < 0 || inner_bytes <= 0) return CO_E_INVAL;
+  if (outer == 0 || idx_len == 0) return CO_OK;
+  if (!src || !idx || !dst) return CO_E_INVAL;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                       (uintptr_t)s_outer | (uintptr_t)s_len | (uintptr_t)inner_bytes;
+  const int64_t units = outer * idx_len;
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* sp = static_cast<const uint8_t*>(src);
+#define CO_GATHER(V, W)                                                                        \
+  hipLaunchKernelGGL(gather_kernel<V>, dim3(grid_for(units * (inner_bytes / W), 256)),        \
+                     dim3(256), 0, s, sp, outer, src_len, inner_bytes / W, s_outer, s_len, idx, \
+                     idx_len, i_outer, i_len, static_cast<V*>(dst), status)
+  if ((al & 15) == 0) {
+    CO_GATHER(uint4, 16);
+  } else if ((al & 7) == 0) {
+    CO_GATHER(uint2, 8);
+  } else if ((al & 3) == 0) {
+    CO_GATHER(uint32_t, 4);
+  } else {
+    CO_GATHER(uint8_t, 1);
+  }
+#undef CO_GATHER
+  return launch_status();
+}
+
+extern "C" int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t* flag,
+                             void* stream) {
+  if (n < 0 || !flag) return CO_E_INVAL;
+  hipError_t e = hipMemsetAsync(flag, 0, sizeof(int32_t), (hipStream_t)stream);
+  if (e != hipSuccess) return (int)e;
+  if (n == 0) return CO_OK;
+  if (!x) return CO_E_INVAL;
+  hipLaunchKernelGGL(any_eq_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0,
+                     (hipStream_t)stream, x, n, value, flag);
+  return launch_status();
+}
+
+extern "C" int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream) {
+  if (n < 0 || !count) return CO_E_INVAL;
+  hipError_t e = hipMemsetAsync(count, 0, sizeof(int32_t), (hipStream_t)stream);
+  if (e != hipSuccess) return (int)e;
+  if (n == 0) return CO_OK;
+  if (!done) return CO_E_INVAL;
+  hipLaunchKernelGGL(count_not_done_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0,
+                     (hipStream_t)stream, done, n, count);
+  return launch_status();
+}

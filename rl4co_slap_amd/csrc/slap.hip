@@ -1,0 +1,222 @@
+// SLAP (storage location assignment) env kernels for gfx950: reset, step
+// (assignment write + location mask) and the per-order pick-tour reward.
+//
+// Step: the 64-instance byte tile of co_tile.hpp for the [B, L] mask (no row
+// count needed: done = i == P-1, slap/env.py:57); the assignment row is copied
+// only when the output is a fresh buffer (the reference clones, env.py:50), and
+// the single element [b, product] is written afterwards by the row's thread.
+//
+// Reward: one wavefront per instance.  Lane s owns pick slot s = (order o, pick k)
+// of the O*K picklist, gathers product -> location -> (x, y) into LDS; lane o then
+// sums its order's closed-tour edges in pick order and lane 0 accumulates the
+// orders in order (slap/env.py:136-142 adds them one by one in f32).
+#include "co_common.hpp"
+#include "co_tile.hpp"
+
+using namespace co;
+
+namespace {
+
+__global__ __launch_bounds__(256) void slap_reset_kernel(int64_t B, int64_t L, int64_t P,
+                                                         uint8_t* mask, float* to_choose,
+                                                         int64_t* it, float* reward,
+                                                         float* ratio) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t k = t0; k < B * L; k += stride) mask[k] = (k % L) != 0;
+  for (int64_t k = t0; k < B * P; k += stride) to_choose[k] = (float)(k % P);
+  if (ratio)
+    for (int64_t k = t0; k < B * L; k += stride) ratio[k] = 0.f;
+  for (int64_t b = t0; b < B; b += stride) {
+    it[b] = 0;
+    reward[b] = 0.f;
+  }
+}
+
+struct SlapRowEpilogue {
+  int P;
+  const float* to_choose;
+  int64_t tc_stride;
+  int32_t* assign_out;
+  const int64_t* i_in;
+  int64_t* i_out;
+  uint8_t* done;
+  uint8_t* reward;
+  int32_t* status;
+  __device__ void operator()(int64_t b, int64_t action, int) const {
+    int64_t p = (int64_t)(int)to_choose[b * tc_stride];  // .to(torch.int), env.py:52
+    if (p < 0) p += P;
+    if (p < 0 || p >= P) {
+      set_status(status, CO_ST_INDEX_RANGE);
+    } else {
+      assign_out[b * P + p] = (int32_t)action;  // .to(torch.int), env.py:53-54
+    }
+    const int64_t iv = i_in[b];
+    done[b] = iv == (int64_t)(P - 1);
+    i_out[b] = iv + 1;
+    reward[b] = 0;
+  }
+};
+
+__global__ __launch_bounds__(256) void slap_step_kernel(int64_t B, int L, const int64_t* action,
+                                                        const uint8_t* mask_in, uint8_t* mask_out,
+                                                        const int32_t* assign_in,
+                                                        SlapRowEpilogue epi, int vec) {
+  // Out-of-place assignment: copy the tile's [rows, P] int32 block first.
+  if (assign_in != epi.assign_out) {
+    const int64_t row0 = (int64_t)blockIdx.x * kTileRows;
+    const int rows = (int)((B - row0) < kTileRows ? (B - row0) : kTileRows);
+    const int64_t n = (int64_t)rows * epi.P;
+    const int32_t* s = assign_in + row0 * epi.P;
+    int32_t* d = epi.assign_out + row0 * epi.P;
+    for (int64_t k = threadIdx.x; k < n; k += kTileThreads) d[k] = s[k];
+    // the epilogue's element write (after the tile's __syncthreads) orders after this copy
+  }
+  mask_clear_tile<false, true>(B, L, action, mask_in, mask_out, epi.status, vec != 0, epi);
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void slap_reward_kernel(
+    int64_t B, int L, int P, int O, int K, const int32_t* assignment, const int64_t* picklist,
+    const float2* locs, float* reward, int32_t* status) {
+  extern __shared__ float s_rew[];
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const int S = O * K;
+  float2* pts = reinterpret_cast<float2*>(s_rew) + w * (S + O);
+  float* olen = reinterpret_cast<float*>(pts + S);
+  for (int64_t b = (int64_t)blockIdx.x * WAVES + w; b < B; b += (int64_t)gridDim.x * WAVES) {
+    const int64_t* prow = picklist + b * (int64_t)S;
+    const int32_t* arow = assignment + b * (int64_t)P;
+    const float2* lrow = locs + b * (int64_t)L;
+    bool range = false;
+    for (int s = lane; s < S; s += 64) {
+      int64_t p = prow[s];
+      if (p < 0) p += P;
+      int64_t loc = 0;
+      if (p < 0 || p >= P) {
+        range = true;
+      } else {
+        loc = arow[p];
+        if (loc < 0) loc += L;
+        if (loc < 0 || loc >= L) {
+          range = true;
+          loc = 0;
+        }
+      }
+      pts[s] = lrow[loc];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // per-order closed tour, edges summed in pick order
+    for (int o = lane; o < O; o += 64) {
+      const float2* op = pts + o * K;
+      float len = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float2 p = op[k], q = op[(k + 1 == K) ? 0 : k + 1];
+        len += edge_len(p.x, p.y, q.x, q.y);
+      }
+      olen[o] = len;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      float total = 0.f;
+      for (int o = 0; o < O; ++o) total += -olen[o];
+      reward[b] = total;
+    }
+    if (__any(range) && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(256) void slap_closest_kernel(int64_t B, int L, const float* dist,
+                                                           const uint8_t* mask, int64_t* out) {
+  const int lane = lane_id();
+  const int64_t wpb = blockDim.x >> 6;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+       b += (int64_t)gridDim.x * wpb) {
+    const float* drow = dist + b * (int64_t)L;
+    const uint8_t* mrow = mask + b * (int64_t)L;
+    float best = __builtin_inff();
+    int bi = 0x7fffffff;
+    for (int c = lane; c < L; c += 64) {
+      const float d = mrow[c] ? drow[c] : __builtin_inff();
+      if (d < best || (d == best && c < bi)) { best = d; bi = c; }
+    }
+    wave_argmin(best, bi);
+    if (lane == 0) out[b] = bi;
+  }
+}
+
+}  // namespace
+
+extern "C" int co_slap_reset(int64_t B, int64_t L, int64_t P, uint8_t* mask, float* to_choose,
+                             int64_t* it, float* reward, float* ratio, void* stream) {
+  if (B < 0 || L <= 0 || P <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!mask || !to_choose || !it || !reward) return CO_E_INVAL;
+  hipLaunchKernelGGL(slap_reset_kernel, dim3(grid_for(B * L, 256)), dim3(256), 0,
+                     (hipStream_t)stream, B, L, P, mask, to_choose, it, reward, ratio);
+  return launch_status();
+}
+
+extern "C" int co_slap_step(int64_t B, int64_t L, int64_t P, const int64_t* action,
+                            const float* to_choose, int64_t tc_stride, const int32_t* assign_in,
+                            int32_t* assign_out, const uint8_t* mask_in, uint8_t* mask_out,
+                            const int64_t* i_in, int64_t* i_out, uint8_t* done, uint8_t* reward,
+                            int32_t* status, void* stream) {
+  if (B < 0 || L <= 0 || P <= 0 || L > (1 << 30)) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!action || !to_choose || !assign_in || !assign_out || !mask_in || !mask_out || !i_in ||
+      !i_out || !done || !reward)
+    return CO_E_INVAL;
+  SlapRowEpilogue epi{(int)P, to_choose, tc_stride, assign_out, i_in, i_out, done, reward,
+                      status};
+  const unsigned grid = (unsigned)((B + kTileRows - 1) / kTileRows);
+  hipLaunchKernelGGL(slap_step_kernel, dim3(grid), dim3(kTileThreads), 0, (hipStream_t)stream, B,
+                     (int)L, action, mask_in, mask_out, assign_in, epi,
+                     tile_vec_ok(mask_in, mask_out));
+  return launch_status();
+}
+
+extern "C" int co_slap_reward(int64_t B, int64_t L, int64_t P, int64_t O, int64_t K,
+                              const int32_t* assignment, const int64_t* picklist,
+                              const float* locs, float* reward, int32_t* status, void* stream) {
+  if (B < 0 || L <= 0 || P <= 0 || O <= 0 || K <= 0 || O * K > (1 << 16)) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!assignment || !picklist || !locs || !reward) return CO_E_INVAL;
+  if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  const size_t per_wave = (size_t)(O * K) * sizeof(float2) + (size_t)O * sizeof(float) + 8;
+  int waves = 4;
+  while (waves > 1 && per_wave * waves > 64 * 1024) waves >>= 1;
+  if (per_wave > 64 * 1024) return CO_E_INVAL;
+  const dim3 grid(grid_for(B, waves, 256 * 32));
+  // stride per wave in float2 units is (S + O); keep the LDS request consistent with it
+  const size_t shmem = (size_t)waves * (size_t)(O * K + O) * sizeof(float2);
+  const float2* l2 = reinterpret_cast<const float2*>(locs);
+  switch (waves) {
+    case 4:
+      hipLaunchKernelGGL(slap_reward_kernel<4>, grid, dim3(256), shmem, (hipStream_t)stream, B,
+                         (int)L, (int)P, (int)O, (int)K, assignment, picklist, l2, reward, status);
+      break;
+    case 2:
+      hipLaunchKernelGGL(slap_reward_kernel<2>, grid, dim3(128), shmem, (hipStream_t)stream, B,
+                         (int)L, (int)P, (int)O, (int)K, assignment, picklist, l2, reward, status);
+      break;
+    default:
+      hipLaunchKernelGGL(slap_reward_kernel<1>, grid, dim3(64), shmem, (hipStream_t)stream, B,
+                         (int)L, (int)P, (int)O, (int)K, assignment, picklist, l2, reward, status);
+  }
+  return launch_status();
+}
+
+extern "C" int co_slap_closest_free_action(int64_t B, int64_t L, const float* dist,
+                                           const uint8_t* mask, int64_t* out, void* stream) {
+  if (B < 0 || L <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!dist || !mask || !out) return CO_E_INVAL;
+  hipLaunchKernelGGL(slap_closest_kernel, dim3(grid_for(B, 4, 256 * 32)), dim3(256), 0,
+                     (hipStream_t)stream, B, (int)L, dist, mask, out);
+  return launch_status();
+}

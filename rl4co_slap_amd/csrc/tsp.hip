@@ -1,0 +1,208 @@
+// TSP env kernels for gfx950: reset, step (mask scatter + done), episode reward,
+// and the nearest-unvisited bench policy.
+//
+// Step layout: one 256-thread workgroup owns a tile of 64 consecutive instances.
+// The tile's action_mask bytes (64*N, always a multiple of 16) are streamed with
+// 16-byte coalesced loads/stores; each thread clears the byte of its chunk that
+// matches its row's action and counts surviving bytes into a per-row LDS counter
+// (done = count == 0).  Row scalars (action, i, first_node, ...) are read/written
+// coalesced by the first 64 threads.
+//
+// Reward layout: one wavefront per instance (grid-stride); lanes walk the tour,
+// gather both edge endpoints (L1/L2-resident row), accumulate edge lengths in
+// f64 and wave-reduce; the permutation check uses a per-wave LDS bitmap.
+#include "co_common.hpp"
+#include "co_tile.hpp"
+
+using namespace co;
+
+namespace {
+
+__global__ __launch_bounds__(256) void tsp_reset_kernel(int64_t B, int64_t N, uint8_t* mask,
+                                                        int64_t* first, int64_t* cur,
+                                                        int64_t* it, float* reward) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nbytes = B * N;
+  // 16-byte fill of the mask (the tail is byte-filled).
+  const int64_t nvec = nbytes >> 4;
+  uint4 ones = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+  for (int64_t k = t0; k < nvec; k += stride) reinterpret_cast<uint4*>(mask)[k] = ones;
+  for (int64_t k = (nvec << 4) + t0; k < nbytes; k += stride) mask[k] = 1;
+  for (int64_t b = t0; b < B; b += stride) {
+    first[b] = 0;
+    cur[b] = 0;
+    it[b] = 0;
+    reward[b] = 0.f;
+  }
+}
+
+struct TspRowEpilogue {
+  const int64_t* i_in;
+  int64_t* i_out;
+  const int64_t* first_in;
+  int64_t* first_out;
+  int64_t* cur_out;
+  uint8_t* done;
+  uint8_t* reward;
+  int take_first;
+  __device__ void operator()(int64_t b, int64_t action, int remaining) const {
+    const int64_t f = take_first ? action : first_in[b];
+    const int64_t iv = i_in[b];
+    first_out[b] = f;
+    i_out[b] = iv + 1;
+    if (cur_out) cur_out[b] = action;
+    done[b] = remaining == 0;
+    reward[b] = 0;
+  }
+};
+
+__global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const int64_t* action,
+                                                       const uint8_t* mask_in, uint8_t* mask_out,
+                                                       TspRowEpilogue epi, int first_mode,
+                                                       const int32_t* first_flag, int32_t* status,
+                                                       int vec) {
+  if (first_mode == 2) epi.take_first = (*first_flag != 0);
+  mask_clear_tile<true>(B, N, action, mask_in, mask_out, status, vec != 0, epi);
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void tsp_reward_kernel(int64_t B, int N, int T,
+                                                                const float2* locs,
+                                                                const int64_t* actions,
+                                                                int64_t sb, int64_t st, int check,
+                                                                float* reward, int32_t* status) {
+  extern __shared__ uint32_t s_bits[];
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  const int words = (T + 31) >> 5;
+  uint32_t* bits = s_bits + w * words;
+  for (int64_t b = (int64_t)blockIdx.x * WAVES + w; b < B; b += (int64_t)gridDim.x * WAVES) {
+    if (check) {
+      for (int k = lane; k < words; k += 64) bits[k] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    const int64_t* arow = actions + b * sb;
+    const float2* lrow = locs + b * (int64_t)N;
+    double acc = 0.0;
+    bool bad = false, range = false;
+    for (int t = lane; t < T; t += 64) {
+      const int64_t a = arow[(int64_t)t * st];
+      const int64_t an = arow[(int64_t)((t + 1 == T) ? 0 : t + 1) * st];
+      if (check) {
+        if (a < 0 || a >= T) {
+          bad = true;
+        } else {
+          const uint32_t bit = 1u << (a & 31);
+          if (atomicOr(&bits[a >> 5], bit) & bit) bad = true;
+        }
+      }
+      if (a < 0 || a >= N || an < 0 || an >= N) {
+        range = true;
+        continue;
+      }
+      const float2 p = lrow[a], q = lrow[an];
+      acc += (double)edge_len(p.x, p.y, q.x, q.y);
+    }
+    acc = wave_sum(acc);
+    if (__any(bad) && lane == 0) set_status(status, CO_ST_INVALID_TOUR);
+    if (__any(range) && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
+    if (lane == 0) reward[b] = -(float)acc;
+  }
+}
+
+// Bench policy: nearest unvisited node to current_node; step 0 -> node 0.
+__global__ __launch_bounds__(256) void tsp_nearest_kernel(int64_t B, int N, const float2* locs,
+                                                          const uint8_t* mask, const int64_t* cur,
+                                                          int first_step, int64_t* out) {
+  const int lane = lane_id();
+  const int64_t wpb = blockDim.x >> 6;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+       b += (int64_t)gridDim.x * wpb) {
+    if (first_step) {
+      if (lane == 0) out[b] = 0;
+      continue;
+    }
+    const float2* lrow = locs + b * (int64_t)N;
+    const uint8_t* mrow = mask + b * (int64_t)N;
+    int64_t c0 = cur[b];
+    c0 = (c0 < 0 || c0 >= N) ? 0 : c0;
+    const float2 p = lrow[c0];
+    float best = __builtin_inff();
+    int bi = 0x7fffffff;
+    for (int c = lane; c < N; c += 64) {
+      float d = __builtin_inff();
+      if (mrow[c]) {
+        const float2 q = lrow[c];
+        d = edge_len(p.x, p.y, q.x, q.y);
+      }
+      if (d < best || (d == best && c < bi)) { best = d; bi = c; }
+    }
+    wave_argmin(best, bi);
+    if (lane == 0) out[b] = bi;
+  }
+}
+
+}  // namespace
+
+extern "C" int co_tsp_reset(int64_t B, int64_t N, uint8_t* mask, int64_t* first, int64_t* cur,
+                            int64_t* it, float* reward, void* stream) {
+  if (B < 0 || N <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!mask || !first || !cur || !it || !reward) return CO_E_INVAL;
+  if (reinterpret_cast<uintptr_t>(mask) & 15) return CO_E_ALIGN;
+  hipLaunchKernelGGL(tsp_reset_kernel, dim3(grid_for(B * N / 16 + B, 256)), dim3(256), 0,
+                     (hipStream_t)stream, B, N, mask, first, cur, it, reward);
+  return launch_status();
+}
+
+extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const uint8_t* mask_in,
+                           uint8_t* mask_out, const int64_t* i_in, int64_t* i_out,
+                           const int64_t* first_in, int64_t* first_out, int64_t* current_out,
+                           uint8_t* done, uint8_t* reward, int first_mode,
+                           const int32_t* first_flag, int32_t* status, void* stream) {
+  if (B < 0 || N <= 0 || N > (1 << 30)) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!action || !mask_in || !mask_out || !i_in || !i_out || !first_out || !done || !reward)
+    return CO_E_INVAL;
+  if (first_mode < 0 || first_mode > 2) return CO_E_MODE;
+  if (first_mode != 1 && !first_in) return CO_E_INVAL;
+  if (first_mode == 2 && !first_flag) return CO_E_INVAL;
+  const int vec = tile_vec_ok(mask_in, mask_out);
+  TspRowEpilogue epi{i_in, i_out, first_in, first_out, current_out, done, reward,
+                     first_mode == 1};
+  const unsigned grid = (unsigned)((B + kTileRows - 1) / kTileRows);
+  hipLaunchKernelGGL(tsp_step_kernel, dim3(grid), dim3(kTileThreads), 0, (hipStream_t)stream, B,
+                     (int)N, action, mask_in, mask_out, epi, first_mode, first_flag, status, vec);
+  return launch_status();
+}
+
+extern "C" int co_tsp_reward(int64_t B, int64_t N, int64_t T, const float* locs,
+                             const int64_t* actions, int64_t sb, int64_t st, int check,
+                             float* reward, int32_t* status, void* stream) {
+  if (B < 0 || N <= 0 || T <= 0 || T > (1 << 24)) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!locs || !actions || !reward || (check && !status)) return CO_E_INVAL;
+  if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  const size_t words = (size_t)((T + 31) / 32);
+  constexpr int W = 4;
+  const size_t shmem = check ? W * words * sizeof(uint32_t) : 0;
+  if (shmem > 64 * 1024) return CO_E_INVAL;
+  hipLaunchKernelGGL(tsp_reward_kernel<W>, dim3(grid_for(B, W, 256 * 32)), dim3(W * 64), shmem,
+                     (hipStream_t)stream, B, (int)N, (int)T,
+                     reinterpret_cast<const float2*>(locs), actions, sb, st, check, reward,
+                     status);
+  return launch_status();
+}
+
+extern "C" int co_tsp_nearest_action(int64_t B, int64_t N, const float* locs,
+                                     const uint8_t* mask, const int64_t* cur, int first_step,
+                                     int64_t* out, void* stream) {
+  if (B < 0 || N <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!out || (!first_step && (!locs || !mask || !cur))) return CO_E_INVAL;
+  hipLaunchKernelGGL(tsp_nearest_kernel, dim3(grid_for(B, 4, 256 * 32)), dim3(256), 0,
+                     (hipStream_t)stream, B, (int)N, reinterpret_cast<const float2*>(locs), mask,
+                     cur, first_step, out);
+  return launch_status();
+}

@@ -1,0 +1,186 @@
+"""``RL4COEnvBase`` surface for the HIP env engine.
+
+Mirrors ``rl4co/envs/common/base.py:19-333`` (constructor kwargs, ``step``/``reset``
+dispatch, ``get_reward`` wrapper, multistart helpers, dataset plumbing) without
+TorchRL: ``reset`` reproduces TorchRL's merge of the ``_reset`` keys into the input
+td plus ``done``/``terminated`` zeros ``[*B, 1]`` (the td dump of
+``examples/test_slap.ipynb`` cell 13 shows both).
+
+Differences from the reference, all deliberate:
+* ``device`` defaults to ``"cuda"`` when a HIP device is present (the reference
+  defaults to ``"cpu"``); the step/reward functions run only on the device.
+* every tensor the reference allocates on the CPU by accident
+  (``slap/env.py:107,114,135``, ``tsp/env.py:117``) lives on the td's device.
+* data-dependent errors raised synchronously by the reference inside ``_step``
+  (out-of-range scatter index) are recorded in a device status word and raised at
+  the next ``get_reward``/``check_status`` (no per-step host sync).
+"""
+from __future__ import annotations
+
+import abc
+import os
+import weakref
+from typing import Iterable, Optional
+
+import torch
+
+from .. import _native as nat
+from ..td import TensorDict
+from ..utils.ops import get_num_starts, select_start_nodes
+
+
+def _default_device():
+    return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+class RL4COEnvBase(metaclass=abc.ABCMeta):
+    batch_locked = False
+    name = "base"
+
+    def __init__(self, *, data_dir: str = "data/", train_file: str = None, val_file: str = None,
+                 test_file: str = None, val_dataloader_names: list = None,
+                 test_dataloader_names: list = None, check_solution: bool = True,
+                 dataset_cls: callable = None, seed: int = None, device: str = None,
+                 batch_size: torch.Size = None, run_type_checks: bool = False,
+                 allow_done_after_reset: bool = False, _torchrl_mode: bool = False, **kwargs):
+        kwargs.pop("name", None)
+        if kwargs:
+            raise TypeError(f"Unused keyword arguments: {', '.join(kwargs)}")
+        self.device = torch.device(device if device is not None else _default_device())
+        self.batch_size = torch.Size([] if batch_size is None else batch_size)
+        self.data_dir = data_dir
+        self.train_file = os.path.join(data_dir, train_file) if train_file is not None else None
+        self._torchrl_mode = _torchrl_mode
+        self.dataset_cls = dataset_cls
+
+        def files(f):
+            if f is None:
+                return None
+            if isinstance(f, Iterable) and not isinstance(f, str):
+                return [os.path.join(data_dir, x) for x in f]
+            return os.path.join(data_dir, f)
+
+        self.val_file, self.test_file = files(val_file), files(test_file)
+        self.val_dataloader_names = val_dataloader_names
+        self.test_dataloader_names = test_dataloader_names
+        self.check_solution = check_solution
+        if seed is None:
+            seed = torch.empty((), dtype=torch.int64).random_().item()
+        self.set_seed(seed)
+        # host-side knowledge of td["i"] tensors this env produced: tensor -> (version, value)
+        self._i_known = weakref.WeakKeyDictionary()
+
+    # -- seeding (base.py:288-291) ---------------------------------------------
+    def set_seed(self, seed: Optional[int]):
+        self._set_seed(seed)
+        return seed
+
+    def _set_seed(self, seed: Optional[int]):
+        self.rng = torch.manual_seed(seed)
+
+    # -- step / reset (base.py:121-143) ----------------------------------------
+    def step(self, td: TensorDict):
+        if self._torchrl_mode:
+            nxt = self._step(td.clone())
+            td.set("next", nxt)
+            return td
+        td = self._step(td)
+        return {"next": td}
+
+    def reset(self, td: Optional[TensorDict] = None, batch_size=None) -> TensorDict:
+        if batch_size is None:
+            batch_size = self.batch_size if td is None else td.batch_size
+        if td is None or td.is_empty():
+            td = self.generator(batch_size=batch_size)
+        batch_size = [batch_size] if isinstance(batch_size, int) else list(batch_size)
+        if td.device is None or td.device != self.device:
+            td = td.to(self.device)
+        out = self._reset(td, batch_size=batch_size)
+        td.update(out)
+        z = torch.zeros((*batch_size, 1), dtype=torch.bool, device=self.device)
+        td.set("done", z)
+        td.set("terminated", torch.zeros_like(z))
+        return td
+
+    @abc.abstractmethod
+    def _step(self, td):
+        raise NotImplementedError
+
+    @abc.abstractmethod
+    def _reset(self, td=None, batch_size=None):
+        raise NotImplementedError
+
+    # -- reward / mask / validity (base.py:182-213) ----------------------------
+    def get_reward(self, td, actions) -> torch.Tensor:
+        """``base.py:182-188``: validity (if ``check_solution``) + reward, fused in one
+        kernel pass; the reference's second validity pass inside ``_get_reward`` is
+        the same predicate and is not repeated."""
+        return self._get_reward(td, actions, check=self.check_solution)
+
+    @abc.abstractmethod
+    def _get_reward(self, td, actions, check: bool = False):
+        raise NotImplementedError
+
+    def get_action_mask(self, td):
+        raise NotImplementedError
+
+    def check_solution_validity(self, td, actions):
+        raise NotImplementedError
+
+    def get_num_starts(self, td):
+        return get_num_starts(td, self.name)
+
+    def select_start_nodes(self, td, num_starts):
+        return select_start_nodes(td, self, num_starts)
+
+    def replace_selected_actions(self, cur_actions, new_actions, selection_mask):
+        raise NotImplementedError
+
+    def local_search(self, td, actions, **kwargs):
+        raise NotImplementedError(f"Local is not implemented yet for {self.name} environment")
+
+    # -- datasets (base.py:236-286) --------------------------------------------
+    def dataset(self, batch_size=[], phase="train", filename=None):
+        f = getattr(self, f"{phase}_file") if filename is None else filename
+        td = self.generator(batch_size) if f is None else self.load_data(f, batch_size)
+        return td if self.dataset_cls is None else self.dataset_cls(td)
+
+    @staticmethod
+    def load_data(fpath, batch_size=[]):
+        import numpy as np
+
+        with np.load(fpath, allow_pickle=False) as z:
+            data = {k: torch.as_tensor(z[k]) for k in z.files}
+        bs = next(iter(data.values())).shape[:1]
+        return TensorDict(data, batch_size=bs)
+
+    def transform(self):
+        return self
+
+    def render(self, *args, **kwargs):
+        raise NotImplementedError
+
+    def to(self, device):
+        if device is None:
+            return self
+        self.device = torch.device(device)
+        return self
+
+    # -- status word -------------------------------------------------------------
+    @staticmethod
+    def raise_for_status(status: torch.Tensor, messages):
+        """Read a device status word (one host sync) and raise the reference's error."""
+        bits = int(status.item())
+        for bit, exc, msg in messages:
+            if bits & bit:
+                raise exc(msg)
+
+    # -- i-tracking for the batch-wide `i.all() == 0` test ------------------------
+    def _remember_i(self, t: torch.Tensor, value: int):
+        self._i_known[t] = (t._version, value)
+
+    def _known_i(self, t: torch.Tensor):
+        rec = self._i_known.get(t)
+        if rec is None or rec[0] != t._version:
+            return None
+        return rec[1]

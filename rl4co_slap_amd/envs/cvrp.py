@@ -1,0 +1,162 @@
+"""CVRP env + generator on the gfx950 kernels (``rl4co/envs/routing/cvrp/``)."""
+from __future__ import annotations
+
+from typing import Callable, Union
+
+import torch
+from torch.distributions import Uniform
+
+from .. import _native as nat
+from ..td import TensorDict
+from .base import RL4COEnvBase
+from .common import Generator, get_sampler
+
+# cvrp/generator.py:15-30 (Kool et al. 2019, Hottung et al. 2022, Kim et al. 2023)
+CAPACITIES = {10: 20.0, 15: 25.0, 20: 30.0, 30: 33.0, 40: 37.0, 50: 40.0, 60: 43.0, 75: 45.0,
+              100: 50.0, 125: 55.0, 150: 60.0, 200: 70.0, 500: 100.0, 1000: 150.0}
+
+
+class CVRPGenerator(Generator):
+    """``cvrp/generator.py:33-143``: depot sampled with the customers when no depot
+    distribution is given; ``demand = (Uniform(min-1, max-1).int() + 1) / capacity``."""
+
+    def __init__(self, num_loc: int = 20, min_loc: float = 0.0, max_loc: float = 1.0,
+                 loc_distribution: Union[int, float, str, type, Callable] = Uniform,
+                 depot_distribution: Union[int, float, str, type, Callable] = None,
+                 min_demand: int = 1, max_demand: int = 10,
+                 demand_distribution: Union[int, float, type, Callable] = Uniform,
+                 vehicle_capacity: float = 1.0, capacity: float = None, **kwargs):
+        self.num_loc, self.min_loc, self.max_loc = num_loc, min_loc, max_loc
+        self.min_demand, self.max_demand = min_demand, max_demand
+        self.vehicle_capacity = vehicle_capacity
+        self.loc_sampler = kwargs.get("loc_sampler") or get_sampler(
+            "loc", loc_distribution, min_loc, max_loc, **kwargs)
+        if kwargs.get("depot_sampler") is not None:
+            self.depot_sampler = kwargs["depot_sampler"]
+        else:
+            self.depot_sampler = get_sampler("depot", depot_distribution, min_loc, max_loc, **kwargs) \
+                if depot_distribution is not None else None
+        self.demand_sampler = kwargs.get("demand_sampler") or get_sampler(
+            "demand", demand_distribution, min_demand - 1, max_demand - 1, **kwargs)
+        if capacity is None:
+            capacity = CAPACITIES.get(num_loc)
+        if capacity is None:
+            capacity = CAPACITIES[min(CAPACITIES, key=lambda x: abs(x - num_loc))]
+        self.capacity = capacity
+
+    def _generate(self, batch_size) -> TensorDict:
+        if self.depot_sampler is not None:
+            depot = self.depot_sampler.sample((*batch_size, 2))
+            locs = self.loc_sampler.sample((*batch_size, self.num_loc, 2))
+        else:
+            locs = self.loc_sampler.sample((*batch_size, self.num_loc + 1, 2))
+            depot, locs = locs[..., 0, :], locs[..., 1:, :]
+        demand = self.demand_sampler.sample((*batch_size, self.num_loc))
+        demand = (demand.int() + 1).float()
+        capacity = torch.full((*batch_size, 1), self.capacity)
+        return TensorDict({"locs": locs, "depot": depot, "demand": demand / self.capacity,
+                           "capacity": capacity}, batch_size=batch_size)
+
+
+class CVRPEnv(RL4COEnvBase):
+    """``cvrp/env.py:29-199``: fused step + mask, fused reward + validity."""
+
+    name = "cvrp"
+
+    def __init__(self, generator: CVRPGenerator = None, generator_params: dict = {}, **kwargs):
+        super().__init__(**kwargs)
+        self.generator = generator if generator is not None else CVRPGenerator(**generator_params)
+
+    def _reset(self, td=None, batch_size=None) -> TensorDict:
+        """``cvrp/env.py:107-135``: cat(depot, locs), state zeros, capacity fill and the
+        initial action mask in one kernel."""
+        depot, locs, demand = td["depot"], td["locs"], td["demand"]
+        nat.require_device(depot, locs, demand)
+        depot, locs, demand = depot.contiguous(), locs.contiguous(), demand.contiguous()
+        b, n = demand.shape
+        dev = demand.device
+        locs_out = torch.empty((b, n + 1, 2), dtype=torch.float32, device=dev)
+        cur = torch.empty((b, 1), dtype=torch.int64, device=dev)
+        used = torch.empty((b, 1), dtype=torch.float32, device=dev)
+        vcap = torch.empty((b, 1), dtype=torch.float32, device=dev)
+        visited = torch.empty((b, n + 1), dtype=torch.uint8, device=dev)
+        mask = torch.empty((b, n + 1), dtype=torch.bool, device=dev)
+        nat.call("co_cvrp_reset", b, n, nat.ptr(depot), nat.ptr(locs), nat.ptr(demand),
+                 float(self.generator.vehicle_capacity), nat.ptr(locs_out), nat.ptr(cur),
+                 nat.ptr(used), nat.ptr(vcap), nat.ptr(visited), nat.ptr(mask),
+                 nat.stream_of(demand))
+        return TensorDict({"locs": locs_out, "demand": demand, "current_node": cur,
+                           "used_capacity": used, "vehicle_capacity": vcap, "visited": visited,
+                           "action_mask": mask}, batch_size=batch_size)
+
+    def _step(self, td: TensorDict) -> TensorDict:
+        """``cvrp/env.py:73-105`` + ``get_action_mask`` (``:137-149``) in one kernel."""
+        action = td["action"]
+        demand, used, vcap, visited = (td["demand"], td["used_capacity"], td["vehicle_capacity"],
+                                       td["visited"])
+        nat.require_device(action, demand, used, vcap, visited)
+        if action.dtype != torch.int64:
+            action = action.long()
+        action, demand, used, vcap, visited = (x.contiguous() for x in
+                                               (action, demand, used, vcap, visited))
+        b, n = demand.shape
+        dev = demand.device
+        used_out = torch.empty_like(used)
+        visited_out = torch.empty_like(visited)
+        cur = torch.empty((b, 1), dtype=torch.int64, device=dev)
+        done = torch.empty(b, dtype=torch.bool, device=dev)
+        reward = torch.empty(b, dtype=torch.bool, device=dev)
+        mask = torch.empty((b, n + 1), dtype=torch.bool, device=dev)
+        nat.call("co_cvrp_step", b, n, nat.ptr(action), nat.ptr(demand), nat.ptr(used),
+                 nat.ptr(used_out), nat.ptr(vcap), nat.ptr(visited), nat.ptr(visited_out),
+                 nat.ptr(cur), nat.ptr(done), nat.ptr(reward), nat.ptr(mask), None,
+                 nat.stream_of(demand))
+        td.update({"current_node": cur, "used_capacity": used_out, "visited": visited_out,
+                   "reward": reward, "done": done, "action_mask": mask})
+        return td
+
+    @staticmethod
+    def get_action_mask(td: TensorDict) -> torch.Tensor:
+        """``cvrp/env.py:137-149``."""
+        demand, used, vcap, visited, cur = (td["demand"], td["used_capacity"],
+                                            td["vehicle_capacity"], td["visited"],
+                                            td["current_node"])
+        nat.require_device(demand, used, vcap, visited, cur)
+        demand, used, vcap, visited, cur = (x.contiguous() for x in (demand, used, vcap, visited, cur))
+        b, n = demand.shape
+        mask = torch.empty((b, n + 1), dtype=torch.bool, device=demand.device)
+        nat.call("co_cvrp_action_mask", b, n, nat.ptr(demand), nat.ptr(used), nat.ptr(vcap),
+                 nat.ptr(visited), nat.ptr(cur), nat.ptr(mask), nat.stream_of(demand))
+        return mask
+
+    def _get_reward(self, td, actions, check: bool = False) -> torch.Tensor:
+        """``cvrp/env.py:151-190``: -tour length through the depot, fused with the
+        validity check and the sequential capacity scan."""
+        locs, demand, vcap = td["locs"], td["demand"], td["vehicle_capacity"]
+        nat.require_device(locs, actions, demand, vcap)
+        locs, demand, vcap = locs.contiguous(), demand.contiguous(), vcap.contiguous()
+        if actions.dtype != torch.int64:
+            actions = actions.long()
+        b, t = actions.shape
+        n = demand.shape[-1]
+        reward = torch.empty(b, dtype=torch.float32, device=locs.device)
+        status = nat.scratch_status(locs.device)
+        nat.call("co_cvrp_reward", b, n, t, nat.ptr(locs), nat.ptr(actions), actions.stride(0),
+                 actions.stride(1), nat.ptr(demand), nat.ptr(vcap), int(check), nat.ptr(reward),
+                 nat.ptr(status), nat.stream_of(locs))
+        msgs = [(nat.ST_INVALID_TOUR, AssertionError, "Invalid tour"),
+                (nat.ST_OVER_CAPACITY, AssertionError, "Used more than capacity")] if check else []
+        msgs.append((nat.ST_INDEX_RANGE, RuntimeError, "index out of range in gather (actions)"))
+        self.raise_for_status(status, msgs)
+        return reward
+
+    def check_solution_validity(self, td, actions):
+        """``cvrp/env.py:162-190``."""
+        self._get_reward(td, actions, check=True)
+
+    @staticmethod
+    def load_data(fpath, batch_size=[]):
+        """``cvrp/env.py:192-199``: normalise demand by capacity."""
+        td = RL4COEnvBase.load_data(fpath, batch_size)
+        td.set("demand", td["demand"] / td["capacity"][:, None])
+        return td

@@ -1,0 +1,143 @@
+"""SLAP (storage location assignment) env + generator on the gfx950 kernels
+(``rl4co/envs/warehousing/slap/``, the fork's warehouse env)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import _native as nat
+from ..td import TensorDict
+from .base import RL4COEnvBase
+from .common import Generator
+
+
+class SLAPGenerator(Generator):
+    """``slap/generator.py:21-155``.
+
+    Same keys, dtypes and RNG streams as the reference: ``freq`` from torch's global
+    RNG (``Uniform(min_freq, max_freq)``, shape ``[*B, P, 1]``), picklists from
+    numpy's global RNG in the reference's draw order (per instance, per order, one
+    ``randint(0, P, size=K)``; drawn here as one ``randint(0, P, size=(B, O, K))``,
+    which consumes the stream identically -- checked in the tests).  The aisle grid
+    and the Manhattan matrices are computed vectorised instead of the reference's
+    ``B x L`` Python loop (values identical: ``x = aisle * inter_aisle_dist`` in
+    double rounded to f32, ``y = loc * inter_loc_dist``).
+    """
+
+    def __init__(self, n_products: int = 20, n_aisles: int = 10, n_locs: int = 10,
+                 inter_loc_dist: float = 1, inter_aisle_dist: float = 2.4, min_freq: int = 1,
+                 max_freq: int = 20, max_orders: int = 20, max_products_in_order: int = 5,
+                 materialize_dist_mat: bool = True):
+        self.n_products, self.n_aisles, self.n_locs = n_products, n_aisles, n_locs
+        self.max_orders, self.max_products_in_order = max_orders, max_products_in_order
+        self.inter_loc_dist, self.inter_aisle_dist = inter_loc_dist, inter_aisle_dist
+        self.min_freq, self.max_freq = min_freq, max_freq
+        self.freq_sampler = torch.distributions.Uniform(low=min_freq, high=max_freq)
+        self.materialize_dist_mat = materialize_dist_mat
+
+    @staticmethod
+    def _get_distance_matrix(locs: torch.Tensor):
+        """``generator.py:51-65`` (Manhattan)."""
+        if locs.dtype not in (torch.float32, torch.float64):
+            locs = locs.to(torch.float32)
+        return torch.sum(torch.abs(locs[..., :, None, :] - locs[..., None, :, :]), dim=-1)
+
+    def grid(self) -> torch.Tensor:
+        total = self.n_aisles * self.n_locs
+        i = np.arange(total)
+        xy = np.stack([(i // self.n_locs) * self.inter_aisle_dist,
+                       (i % self.n_locs) * self.inter_loc_dist], axis=-1)
+        return torch.tensor(xy, dtype=torch.float64).to(torch.float32)
+
+    def _generate(self, batch_size) -> TensorDict:
+        freq = self.freq_sampler.sample((*batch_size, self.n_products, 1))
+        g = self.grid()
+        locs = g.expand(*batch_size, *g.shape).contiguous()
+        dist1 = self._get_distance_matrix(g)
+        depot = dist1[0].expand(*batch_size, dist1.shape[-1]).contiguous()
+        picklist = torch.from_numpy(np.random.randint(
+            0, self.n_products, size=(batch_size[0], self.max_orders, self.max_products_in_order)
+        ).astype(np.int64))
+        data = {"freq": freq, "locs": locs,
+                "assignment": torch.full((*batch_size, self.n_products), -1, dtype=torch.int),
+                "picklist": picklist, "depot_loc_dist": depot}
+        if self.materialize_dist_mat:
+            data["dist_mat"] = dist1.expand(*batch_size, *dist1.shape).contiguous()
+        return TensorDict(data, batch_size=batch_size)
+
+
+class SLAPEnv(RL4COEnvBase):
+    """``slap/env.py:17-152``."""
+
+    name = "slap"
+
+    def __init__(self, generator: SLAPGenerator = None, generator_params: dict = {},
+                 check_solution=False, **kwargs):
+        super().__init__(**kwargs)
+        self.generator = generator if generator is not None else SLAPGenerator(**generator_params)
+        self.check_solution = check_solution
+
+    def _reset(self, td=None, batch_size=None) -> TensorDict:
+        """``slap/env.py:95-129`` in one kernel (``to_choose``/``ratio`` on the device)."""
+        assignment = td["assignment"]
+        nat.require_device(assignment)
+        b = assignment.shape[0]
+        p = td["freq"].shape[-2]
+        l = td["locs"].shape[1]
+        dev = assignment.device
+        mask = torch.empty((b, l), dtype=torch.bool, device=dev)
+        to_choose = torch.empty((b, p), dtype=torch.float32, device=dev)
+        i = torch.empty((b, 1), dtype=torch.int64, device=dev)
+        reward = torch.empty((b, 1), dtype=torch.float32, device=dev)
+        ratio = torch.empty(td["depot_loc_dist"].shape, dtype=torch.float32, device=dev)
+        nat.call("co_slap_reset", b, l, p, nat.ptr(mask), nat.ptr(to_choose), nat.ptr(i),
+                 nat.ptr(reward), nat.ptr(ratio), nat.stream_of(assignment))
+        return TensorDict({"assignment": assignment, "to_choose": to_choose, "i": i,
+                           "ratio": ratio, "action_mask": mask, "reward": reward},
+                          batch_size=batch_size)
+
+    def _step(self, td: TensorDict) -> TensorDict:
+        """``slap/env.py:38-93``: one kernel replaces the clone + advanced-index write +
+        the per-batch Python loop; ``to_choose`` shrinks as a zero-copy view."""
+        action, tc, assign, mask, i = (td["action"], td["to_choose"], td["assignment"],
+                                       td["action_mask"], td["i"])
+        nat.require_device(action, tc, assign, mask, i)
+        if action.dtype != torch.int64:
+            action = action.long()
+        action, assign, mask, i = (x.contiguous() for x in (action, assign, mask, i))
+        b, l = mask.shape
+        p = td["freq"].shape[-2]
+        dev = mask.device
+        assign_out = torch.empty_like(assign)
+        mask_out = torch.empty_like(mask)
+        i_out = torch.empty_like(i)
+        done = torch.empty((b, 1), dtype=torch.bool, device=dev)
+        reward = torch.empty((b, 1), dtype=torch.bool, device=dev)
+        nat.call("co_slap_step", b, l, p, nat.ptr(action), nat.ptr(tc), tc.stride(0),
+                 nat.ptr(assign), nat.ptr(assign_out), nat.ptr(mask), nat.ptr(mask_out),
+                 nat.ptr(i), nat.ptr(i_out), nat.ptr(done), nat.ptr(reward), None,
+                 nat.stream_of(mask))
+        td.update({"assignment": assign_out, "to_choose": tc[..., 1:], "action_mask": mask_out,
+                   "i": i_out, "reward": reward, "done": done})
+        return td
+
+    def _get_reward(self, td, actions=None, check: bool = False) -> torch.Tensor:
+        """``slap/env.py:131-143``: sum over orders of the closed pick tour (``actions``
+        is ignored, as in the reference)."""
+        if check:
+            raise NotImplementedError  # base.py:209-213: SLAP has no validity check
+        assign, picklist, locs = td["assignment"], td["picklist"], td["locs"]
+        nat.require_device(assign, picklist, locs)
+        assign, picklist, locs = assign.contiguous(), picklist.contiguous(), locs.contiguous()
+        b, o, k = picklist.shape
+        reward = torch.empty(b, dtype=torch.float32, device=locs.device)
+        status = nat.scratch_status(locs.device)
+        nat.call("co_slap_reward", b, locs.shape[1], assign.shape[1], o, k, nat.ptr(assign),
+                 nat.ptr(picklist), nat.ptr(locs), nat.ptr(reward), nat.ptr(status),
+                 nat.stream_of(locs))
+        self.raise_for_status(status, [(nat.ST_INDEX_RANGE, IndexError,
+                                        "index out of range in SLAP reward gather")])
+        return reward
+
+    def get_action_mask(self, td):
+        return td["action_mask"]

@@ -1,0 +1,120 @@
+"""TSP env + generator on the gfx950 kernels (``rl4co/envs/routing/tsp/``)."""
+from __future__ import annotations
+
+from typing import Callable, Union
+
+import torch
+from torch.distributions import Uniform
+
+from .. import _native as nat
+from ..td import TensorDict
+from .base import RL4COEnvBase
+from .common import Generator, get_sampler
+
+
+class TSPGenerator(Generator):
+    """``tsp/generator.py:14-60``: ``locs ~ Uniform(min_loc, max_loc)`` drawn from
+    torch's global CPU RNG (seeded by the env), shape ``[*B, num_loc, 2]``."""
+
+    def __init__(self, num_loc: int = 20, min_loc: float = 0.0, max_loc: float = 1.0,
+                 init_sol_type: str = "random",
+                 loc_distribution: Union[int, float, str, type, Callable] = Uniform, **kwargs):
+        self.num_loc, self.min_loc, self.max_loc = num_loc, min_loc, max_loc
+        self.init_sol_type = init_sol_type
+        self.loc_sampler = kwargs.get("loc_sampler") or get_sampler(
+            "loc", loc_distribution, min_loc, max_loc, **kwargs)
+
+    def _generate(self, batch_size) -> TensorDict:
+        locs = self.loc_sampler.sample((*batch_size, self.num_loc, 2))
+        return TensorDict({"locs": locs}, batch_size=batch_size)
+
+
+class TSPEnv(RL4COEnvBase):
+    """``tsp/env.py:29-173`` with ``_step``/``_reset``/``get_reward`` on the device."""
+
+    name = "tsp"
+
+    def __init__(self, generator: TSPGenerator = None, generator_params: dict = {}, **kwargs):
+        super().__init__(**kwargs)
+        self.generator = generator if generator is not None else TSPGenerator(**generator_params)
+
+    def _reset(self, td=None, batch_size=None) -> TensorDict:
+        """``tsp/env.py:95-120``: one fused reset kernel."""
+        locs = td["locs"]
+        nat.require_device(locs)
+        b, n = locs.shape[0], locs.shape[-2]
+        dev = locs.device
+        cur = torch.empty(b, dtype=torch.int64, device=dev)  # first_node aliases it (env.py:113-114)
+        mask = torch.empty((b, n), dtype=torch.bool, device=dev)
+        i = torch.empty((b, 1), dtype=torch.int64, device=dev)
+        reward = torch.empty((b, 1), dtype=torch.float32, device=dev)
+        nat.call("co_tsp_reset", b, n, nat.ptr(mask), nat.ptr(cur), nat.ptr(cur), nat.ptr(i),
+                 nat.ptr(reward), nat.stream_of(locs))
+        self._remember_i(i, 0)
+        return TensorDict({"locs": locs, "first_node": cur, "current_node": cur, "i": i,
+                           "action_mask": mask, "reward": reward}, batch_size=batch_size)
+
+    def _step(self, td: TensorDict) -> TensorDict:
+        """``tsp/env.py:67-93`` in one kernel launch.  ``current_node`` aliases the
+        action tensor exactly as the reference does."""
+        action, mask, i = td["action"], td["action_mask"], td["i"]
+        nat.require_device(action, mask, i)
+        if action.dtype != torch.int64:
+            action = action.long()
+        action, mask, i = action.contiguous(), mask.contiguous(), i.contiguous()
+        b, n = mask.shape
+        dev = mask.device
+        known = self._known_i(td["i"])
+        first_in = td.get("first_node", None)
+        flag = None
+        if known is not None:
+            mode = 1 if known == 0 else 0
+        else:  # unknown provenance: batch-wide any(i == 0) on the device
+            flag = torch.empty(1, dtype=torch.int32, device=dev)
+            nat.call("co_any_eq_i64", nat.ptr(i), i.numel(), 0, nat.ptr(flag), nat.stream_of(i))
+            mode = 2
+        if first_in is None:
+            first_in = action
+        first_in = first_in.contiguous()
+        mask_out = torch.empty_like(mask)
+        i_out = torch.empty_like(i)
+        first_out = torch.empty_like(action)
+        done = torch.empty(b, dtype=torch.bool, device=dev)
+        reward = torch.empty(b, dtype=torch.bool, device=dev)
+        nat.call("co_tsp_step", b, n, nat.ptr(action), nat.ptr(mask), nat.ptr(mask_out),
+                 nat.ptr(i), nat.ptr(i_out), nat.ptr(first_in), nat.ptr(first_out), None,
+                 nat.ptr(done), nat.ptr(reward), mode, nat.ptr(flag), None, nat.stream_of(mask))
+        if known is not None:
+            self._remember_i(i_out, known + 1)
+        td.update({"first_node": first_out, "current_node": td["action"], "i": i_out,
+                   "action_mask": mask_out, "reward": reward, "done": done})
+        return td
+
+    def _get_reward(self, td, actions, check: bool = False) -> torch.Tensor:
+        """``tsp/env.py:157-173``: -tour length, fused with the permutation check."""
+        locs = td["locs"]
+        nat.require_device(locs, actions)
+        locs = locs.contiguous()
+        if actions.dtype != torch.int64:
+            actions = actions.long()
+        b, t = actions.shape
+        reward = torch.empty(b, dtype=torch.float32, device=locs.device)
+        status = nat.scratch_status(locs.device)
+        nat.call("co_tsp_reward", b, locs.shape[-2], t, nat.ptr(locs), nat.ptr(actions),
+                 actions.stride(0), actions.stride(1), int(check), nat.ptr(reward),
+                 nat.ptr(status), nat.stream_of(locs))
+        msgs = [(nat.ST_INVALID_TOUR, AssertionError, "Invalid tour")] if check else []
+        msgs.append((nat.ST_INDEX_RANGE, RuntimeError, "index out of range in gather (actions)"))
+        self.raise_for_status(status, msgs)
+        return reward
+
+    def check_solution_validity(self, td, actions) -> None:
+        """``tsp/env.py:165-173``."""
+        self._get_reward(td, actions, check=True)
+
+    def get_action_mask(self, td):
+        return td["action_mask"]
+
+    def replace_selected_actions(self, cur_actions, new_actions, selection_mask):
+        cur_actions[selection_mask] = new_actions[selection_mask]
+        return cur_actions

@@ -1,0 +1,156 @@
+"""Device-resident rollout engine: a whole env episode (reset -> every step ->
+reward) as a fixed sequence of C-ABI launches on one stream, captured once into a
+HIP graph and replayed.
+
+This is the env-only rollout of ``rl4co/utils/decoding.py:88-109`` with the policy
+in-kernel (teacher-forced actions = Evaluate mode, or a cheap deterministic policy;
+SURVEY.md 8d) and no host synchronisation inside the episode: the reference's
+``while not td["done"].all()`` poll (``constructive/base.py:230``) is replaced by
+the known episode length (TSP: N steps, SLAP: P steps) and, for CVRP, by a chunked
+graph with a device-side not-done count polled between chunks.
+
+Stepwise mode keeps the reference's TensorDict contract in HBM between steps
+(every step reads and writes the full per-instance state: SURVEY.md 8d's
+250 / 733 / 234 bytes per env-step); state buffers ping-pong between two copies.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native as nat
+
+
+class _GraphEpisode:
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.graph = None
+        self.stream = torch.cuda.Stream(self.device)
+
+    def _launch(self, s):  # pragma: no cover - overridden
+        raise NotImplementedError
+
+    def capture(self):
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.stream(self.stream):
+            self._launch(self.stream.cuda_stream)  # warm (loads code objects)
+        self.stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self.stream):
+            self._launch(torch.cuda.current_stream(self.device).cuda_stream)
+        self.graph = g
+        return self
+
+    def run_eager(self):
+        with torch.cuda.stream(self.stream):
+            self._launch(self.stream.cuda_stream)
+
+    def replay(self):
+        if self.graph is None:
+            self.capture()
+        self.graph.replay()
+
+
+class TSPStepwiseEpisode(_GraphEpisode):
+    """Reset + N x co_tsp_step (+ optional in-kernel nearest policy) + co_tsp_reward."""
+
+    def __init__(self, locs: torch.Tensor, actions: torch.Tensor = None, policy: str = "teacher",
+                 check: bool = True):
+        super().__init__(locs.device)
+        b, n, _ = locs.shape
+        self.b, self.n, self.policy, self.check = b, n, policy, check
+        d = locs.device
+        self.locs = locs.contiguous()
+        if policy == "teacher":
+            assert actions is not None and actions.shape == (b, n)
+            self.acts = actions.t().contiguous()  # step-major: each step's action is a [B] row
+        else:
+            self.acts = torch.empty((n, b), dtype=torch.int64, device=d)
+        self.mask = [torch.empty((b, n), dtype=torch.bool, device=d) for _ in range(2)]
+        self.i = [torch.empty((b, 1), dtype=torch.int64, device=d) for _ in range(2)]
+        self.first = [torch.empty(b, dtype=torch.int64, device=d) for _ in range(2)]
+        self.cur = torch.empty(b, dtype=torch.int64, device=d)
+        self.done = torch.empty(b, dtype=torch.bool, device=d)
+        self.step_reward = torch.empty(b, dtype=torch.bool, device=d)
+        self.reset_reward = torch.empty((b, 1), dtype=torch.float32, device=d)
+        self.reward = torch.empty(b, dtype=torch.float32, device=d)
+        self.status = torch.zeros(1, dtype=torch.int32, device=d)
+
+    def _launch(self, s):
+        b, n = self.b, self.n
+        nat.call("co_tsp_reset", b, n, nat.ptr(self.mask[0]), nat.ptr(self.first[0]),
+                 nat.ptr(self.cur), nat.ptr(self.i[0]), nat.ptr(self.reset_reward), s)
+        for t in range(n):
+            src, dst = t & 1, (t + 1) & 1
+            a = self.acts[t]
+            if self.policy == "nearest":
+                nat.call("co_tsp_nearest_action", b, n, nat.ptr(self.locs), nat.ptr(self.mask[src]),
+                         nat.ptr(self.cur), int(t == 0), nat.ptr(a), s)
+            nat.call("co_tsp_step", b, n, nat.ptr(a), nat.ptr(self.mask[src]),
+                     nat.ptr(self.mask[dst]), nat.ptr(self.i[src]), nat.ptr(self.i[dst]),
+                     nat.ptr(self.first[src]), nat.ptr(self.first[dst]), nat.ptr(self.cur),
+                     nat.ptr(self.done), nat.ptr(self.step_reward), 1 if t == 0 else 0, None,
+                     nat.ptr(self.status), s)
+        nat.call("co_tsp_reward", b, n, n, nat.ptr(self.locs), nat.ptr(self.acts), 1, b,
+                 int(self.check), nat.ptr(self.reward), nat.ptr(self.status), s)
+
+    def final_state(self):
+        k = self.n & 1
+        return {"action_mask": self.mask[k], "i": self.i[k], "first_node": self.first[k],
+                "current_node": self.cur, "done": self.done, "reward": self.reward,
+                "actions": self.acts.t()}
+
+
+class SLAPStepwiseEpisode(_GraphEpisode):
+    """Reset + P x co_slap_step (in-place assignment) + co_slap_reward."""
+
+    def __init__(self, td, actions=None, policy: str = "teacher"):
+        locs = td["locs"]
+        super().__init__(locs.device)
+        d = locs.device
+        b, l = locs.shape[0], locs.shape[1]
+        p = td["freq"].shape[-2]
+        self.b, self.l, self.p, self.policy = b, l, p, policy
+        self.locs = locs.contiguous()
+        self.picklist = td["picklist"].contiguous()
+        self.depot_dist = td["depot_loc_dist"].contiguous()
+        self.assign0 = td["assignment"].contiguous()
+        self.assign = torch.empty_like(self.assign0)
+        if policy == "teacher":
+            self.acts = actions.t().contiguous()
+        else:
+            self.acts = torch.empty((p, b), dtype=torch.int64, device=d)
+        self.mask = [torch.empty((b, l), dtype=torch.bool, device=d) for _ in range(2)]
+        self.i = [torch.empty((b, 1), dtype=torch.int64, device=d) for _ in range(2)]
+        self.to_choose = torch.empty((b, p), dtype=torch.float32, device=d)
+        self.ratio = torch.empty((b, l), dtype=torch.float32, device=d)
+        self.done = torch.empty((b, 1), dtype=torch.bool, device=d)
+        self.step_reward = torch.empty((b, 1), dtype=torch.bool, device=d)
+        self.reset_reward = torch.empty((b, 1), dtype=torch.float32, device=d)
+        self.reward = torch.empty(b, dtype=torch.float32, device=d)
+        self.status = torch.zeros(1, dtype=torch.int32, device=d)
+
+    def _launch(self, s):
+        b, l, p = self.b, self.l, self.p
+        nat.call("co_slap_reset", b, l, p, nat.ptr(self.mask[0]), nat.ptr(self.to_choose),
+                 nat.ptr(self.i[0]), nat.ptr(self.reset_reward), nat.ptr(self.ratio), s)
+        # the generator's -1 assignment is the episode's starting state
+        self.assign.copy_(self.assign0, non_blocking=True)
+        for t in range(p):
+            src, dst = t & 1, (t + 1) & 1
+            a = self.acts[t]
+            if self.policy == "closest":
+                nat.call("co_slap_closest_free_action", b, l, nat.ptr(self.depot_dist),
+                         nat.ptr(self.mask[src]), nat.ptr(a), s)
+            tc = self.to_choose[:, t:]
+            nat.call("co_slap_step", b, l, p, nat.ptr(a), nat.ptr(tc), p, nat.ptr(self.assign),
+                     nat.ptr(self.assign), nat.ptr(self.mask[src]), nat.ptr(self.mask[dst]),
+                     nat.ptr(self.i[src]), nat.ptr(self.i[dst]), nat.ptr(self.done),
+                     nat.ptr(self.step_reward), nat.ptr(self.status), s)
+        nat.call("co_slap_reward", b, l, p, self.picklist.shape[1], self.picklist.shape[2],
+                 nat.ptr(self.assign), nat.ptr(self.picklist), nat.ptr(self.locs),
+                 nat.ptr(self.reward), nat.ptr(self.status), s)
+
+    def final_state(self):
+        k = self.p & 1
+        return {"action_mask": self.mask[k], "i": self.i[k], "assignment": self.assign,
+                "done": self.done, "reward": self.reward, "actions": self.acts.t()}

@@ -1,0 +1,220 @@
+"""Decoding strategies (``rl4co/utils/decoding.py``) on the fused gfx950 decode step.
+
+``DecodingStrategy.step`` issues one ``co_decode_step`` launch per decode step:
+tanh clipping, masking, temperature, ``log_softmax``, greedy argmax / Philox
+sampling / evaluate, and the logprob gather.  The greedy/sampling feasibility
+assertion (``decoding.py:376-379,393-395``) is recorded in a device status word
+and raised once in ``post_decoder_hook`` instead of synchronising every step.
+Top-k / top-p filtering, beam search and multi-sampling are out of scope
+(SURVEY.md section 8f).
+"""
+from __future__ import annotations
+
+import abc
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _native as nat
+from ..td import TensorDict
+from .ops import batchify, gather_by_index, unbatchify, unbatchify_and_gather
+
+_MODES = {"greedy": 0, "sampling": 1, "evaluate": 2}
+
+
+def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, action=None,
+                return_full=False, seed=None, offset=0, status=None):
+    """One fused decode step.  Returns ``(action[B], logp[B], full_logprobs or None)``."""
+    nat.require_device(logits, mask, action)
+    if logits.dtype != torch.float32:
+        logits = logits.float()
+    if logits.stride(-1) != 1:
+        logits = logits.contiguous()
+    b, n = logits.shape
+    dev = logits.device
+    if mask is not None:
+        mask = mask.contiguous()
+    act_out = torch.empty(b, dtype=torch.int64, device=dev)
+    logp = torch.empty(b, dtype=torch.float32, device=dev)
+    full = torch.empty((b, n), dtype=torch.float32, device=dev) if return_full else None
+    if action is not None:
+        action = action.long().contiguous()
+    if seed is None:
+        seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
+    nat.call("co_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
+             float(tanh_clipping), float(temperature), _MODES[mode], nat.ptr(action),
+             nat.ptr(act_out), nat.ptr(logp), nat.ptr(full), seed, offset, nat.ptr(status),
+             nat.stream_of(logits))
+    return act_out, logp, full
+
+
+def process_logits(logits, mask=None, temperature: float = 1.0, top_p: float = 0.0,
+                   top_k: int = 0, tanh_clipping: float = 0, mask_logits: bool = True):
+    """``decoding.py:141-191`` -> full log-probabilities (top-k/top-p unsupported)."""
+    if top_k > 0 or top_p > 0:
+        raise NotImplementedError("top-k / top-p filtering is not on the MI355X hot path")
+    if mask_logits:
+        assert mask is not None, "mask must be provided if mask_logits is True"
+    _, _, full = decode_step(logits, mask if mask_logits else None, "greedy", temperature,
+                             tanh_clipping, return_full=True)
+    return full
+
+
+def get_log_likelihood(logprobs, actions=None, mask=None, return_sum: bool = True):
+    """``decoding.py:39-65``."""
+    if actions is not None and logprobs.dim() == 3:
+        logprobs = logprobs.gather(-1, actions.unsqueeze(-1)).squeeze(-1)
+    if mask is not None:
+        logprobs[~mask] = 0
+    assert (logprobs > -1000).data.all(), "Logprobs should not be -inf, check sampling procedure!"
+    return logprobs.sum(1) if return_sum else logprobs
+
+
+def random_policy(td):
+    """``decoding.py:81-85``."""
+    action = torch.multinomial(td["action_mask"].float(), 1).squeeze(-1)
+    td.set("action", action)
+    return td
+
+
+def rollout(env, td, policy, max_steps: int = None):
+    """``decoding.py:88-109``."""
+    max_steps = float("inf") if max_steps is None else max_steps
+    actions, steps = [], 0
+    while not td["done"].all():
+        td = policy(td)
+        actions.append(td["action"])
+        td = env.step(td)["next"]
+        steps += 1
+        if steps > max_steps:
+            break
+    acts = torch.stack(actions, dim=1)
+    return env.get_reward(td, acts), td, acts
+
+
+class DecodingStrategy(metaclass=abc.ABCMeta):
+    """``decoding.py:194-407``."""
+
+    name = "base"
+
+    def __init__(self, temperature: float = 1.0, top_p: float = 0.0, top_k: int = 0,
+                 mask_logits: bool = True, tanh_clipping: float = 0, multistart: bool = False,
+                 multisample: bool = False, num_starts: Optional[int] = None,
+                 select_start_nodes_fn: Optional[callable] = None,
+                 improvement_method_mode: bool = False, select_best: bool = False,
+                 store_all_logp: bool = False, key: str = "action", **kwargs):
+        if top_k > 0 or top_p > 0:
+            raise NotImplementedError("top-k / top-p filtering is not on the MI355X hot path")
+        self.temperature, self.top_p, self.top_k = temperature, top_p, top_k
+        self.mask_logits, self.tanh_clipping = mask_logits, tanh_clipping
+        self.multistart, self.multisample = multistart, multisample
+        self.num_starts, self.select_start_nodes_fn = num_starts, select_start_nodes_fn
+        self.improvement_method_mode, self.select_best = improvement_method_mode, select_best
+        self.store_all_logp, self.key = store_all_logp, key
+        self.actions, self.logprobs = [], []
+        self._status = None
+        self._step_idx = 0
+
+    def pre_decoder_hook(self, td, env, action=None):
+        """``decoding.py:265-313``."""
+        if self.multistart or self.multisample:
+            if self.num_starts is None:
+                self.num_starts = env.get_num_starts(td)
+        else:
+            self.num_starts = 0
+        if self.num_starts >= 1:
+            if self.multistart:
+                if action is None:
+                    if self.select_start_nodes_fn is not None:
+                        action = self.select_start_nodes_fn(td, env, self.num_starts)
+                    else:
+                        action = env.select_start_nodes(td, num_starts=self.num_starts)
+                td = batchify(td, self.num_starts)
+                td.set("action", action)
+                td = env.step(td)["next"]
+                lp = torch.zeros_like(td["action_mask"]) if self.store_all_logp else \
+                    torch.zeros_like(action, device=td.device)
+                self.logprobs.append(lp)
+                self.actions.append(action)
+            else:
+                td = batchify(td, self.num_starts)
+        return td, env, self.num_starts
+
+    def post_decoder_hook(self, td, env):
+        """``decoding.py:315-325`` + the deferred feasibility assertion."""
+        assert len(self.logprobs) > 0, \
+            "No logprobs were collected because all environments were done. Check your initial state"
+        if self._status is not None and int(self._status.item()) & nat.ST_INFEASIBLE:
+            raise AssertionError("infeasible action selected")
+        logprobs = torch.stack(self.logprobs, 1)
+        actions = torch.stack(self.actions, 1)
+        if self.num_starts > 0 and self.select_best:
+            logprobs, actions, td, env = self._select_best(logprobs, actions, td, env)
+        return logprobs, actions, td, env
+
+    def step(self, logits, mask, td: TensorDict = None, action=None, env=None, **kwargs):
+        """``decoding.py:327-369`` as one fused launch."""
+        if not self.mask_logits:
+            mask = None
+        if self._status is None:
+            self._status = nat.scratch_status(logits.device)
+        mode = self._mode()
+        act_in = action if mode == "evaluate" else None
+        sel, logp, full = decode_step(logits, mask, mode, self.temperature, self.tanh_clipping,
+                                      action=act_in, return_full=self.store_all_logp,
+                                      offset=self._step_idx, status=self._status)
+        self._step_idx += 1
+        if mode == "evaluate":
+            sel = action
+        if self.improvement_method_mode:
+            return (full if full is not None else logp), sel
+        out_lp = full if self.store_all_logp else logp
+        td.set(self.key, sel)
+        self.actions.append(sel)
+        self.logprobs.append(out_lp)
+        return td
+
+    @abc.abstractmethod
+    def _mode(self) -> str:
+        raise NotImplementedError
+
+    def _select_best(self, logprobs, actions, td, env):
+        """``decoding.py:399-407``."""
+        rewards = env.get_reward(td, actions)
+        _, max_idxs = unbatchify(rewards, self.num_starts).max(dim=-1)
+        actions = unbatchify_and_gather(actions, max_idxs, self.num_starts)
+        logprobs = unbatchify_and_gather(logprobs, max_idxs, self.num_starts)
+        td = unbatchify(td, self.num_starts)
+        td = TensorDict({k: gather_by_index(v, max_idxs, dim=1) for k, v in td.items()},
+                        batch_size=max_idxs.shape)
+        return logprobs, actions, td, env
+
+
+class Greedy(DecodingStrategy):
+    name = "greedy"
+
+    def _mode(self):
+        return "greedy"
+
+
+class Sampling(DecodingStrategy):
+    name = "sampling"
+
+    def _mode(self):
+        return "sampling"
+
+
+class Evaluate(DecodingStrategy):
+    name = "evaluate"
+
+    def _mode(self):
+        return "evaluate"
+
+
+def get_decoding_strategy(decoding_strategy, **config):
+    """``decoding.py:17-36`` (beam search / multisampling are out of scope)."""
+    registry = {"greedy": Greedy, "sampling": Sampling, "multistart_greedy": Greedy,
+                "multistart_sampling": Sampling, "evaluate": Evaluate}
+    if "multistart" in decoding_strategy:
+        config["multistart"] = True
+    return registry.get(decoding_strategy, Sampling)(**config)

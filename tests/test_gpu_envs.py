@@ -1,0 +1,239 @@
+"""GPU parity: the HIP env kernels (through the C ABI, via the env classes) against
+the CPU oracle on identical seeded instances and actions.
+
+Bar: bit-exact for masks / indices / bool and int state and the CVRP capacity
+floats; episode rewards within |gpu - ref| <= 1e-5 * max(1, |ref|) (the summation
+order of 100 f32 edges differs from ATen's vectorised CPU reduction)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.envs import (CVRPOracle, SLAPOracle, TSPOracle, cvrp_nearest_action,
+                         slap_closest_free_action, tsp_nearest_action)
+from oracle.td import TD
+from rl4co_slap_amd.envs import CVRPEnv, SLAPEnv, TSPEnv
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def assert_reward_close(got, ref):
+    got, ref = got.cpu(), ref.cpu()
+    tol = RTOL * torch.clamp(ref.abs(), min=1.0)
+    assert ((got - ref).abs() <= tol).all(), (got - ref).abs().max()
+
+
+def assert_same(a, b, key):
+    a = a.cpu()
+    assert a.dtype == b.dtype, (key, a.dtype, b.dtype)
+    assert a.shape == b.shape, (key, a.shape, b.shape)
+    assert torch.equal(a, b), key
+
+
+def rand_perm_actions(b, n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(b, n, generator=g).argsort(1)
+
+
+@pytest.mark.parametrize("b,n", [(1, 5), (63, 20), (128, 20), (200, 37), (64, 100), (130, 100), (7, 3)])
+def test_tsp_teacher_forced_episode(dev, b, n):
+    ref_env = TSPOracle(num_loc=n, seed=1234)
+    td_ref = ref_env.reset(batch_size=[b])
+    env = TSPEnv(generator_params=dict(num_loc=n), seed=99, device=dev)
+    import rl4co_slap_amd as ra
+
+    td = env.reset(ra.TensorDict({"locs": td_ref["locs"].clone()}, [b]))
+    for k in ("action_mask", "first_node", "current_node", "i", "done", "terminated"):
+        assert_same(td[k], td_ref[k], k)
+    acts = rand_perm_actions(b, n, 4321)
+    for t in range(n):
+        td_ref["action"] = acts[:, t].clone()
+        td_ref = ref_env.step(td_ref)["next"]
+        td["action"] = acts[:, t].to(dev)
+        td = env.step(td)["next"]
+        for k in ("action_mask", "first_node", "current_node", "i", "done", "reward"):
+            assert_same(td[k], td_ref[k], f"{k}@{t}")
+    r_ref = ref_env.get_reward(td_ref, acts)
+    r = env.get_reward(td, acts.to(dev))
+    assert_reward_close(r, r_ref)
+
+
+def test_tsp_invalid_tour_raises(dev):
+    env = TSPEnv(generator_params=dict(num_loc=6), seed=1, device=dev)
+    td = env.reset(batch_size=[4])
+    acts = torch.arange(6).repeat(4, 1)
+    acts[2, 3] = 1
+    with pytest.raises(AssertionError, match="Invalid tour"):
+        env.get_reward(td, acts.to(dev))
+    env.check_solution = False
+    env.get_reward(td, acts.to(dev))  # no check -> no error
+
+
+def test_tsp_first_node_unknown_i_uses_device_test(dev):
+    # td["i"] of foreign provenance -> batch-wide any(i == 0) on the device (tsp/env.py:70)
+    ref_env = TSPOracle(num_loc=4, seed=0)
+    env = TSPEnv(generator_params=dict(num_loc=4), seed=0, device=dev)
+    for ivals, expect in [([[0], [5]], [2, 0]), ([[3], [5]], [1, 1])]:
+        td = env.reset(batch_size=[2])
+        td["i"] = torch.tensor(ivals, device=dev)
+        td["first_node"] = torch.tensor([1, 1], device=dev)
+        td["action"] = torch.tensor([2, 0], device=dev)
+        td = env.step(td)["next"]
+        assert td["first_node"].tolist() == expect
+        assert td["i"].cpu().squeeze(-1).tolist() == [v[0] + 1 for v in ivals]
+
+
+def test_tsp_nearest_policy_episode(dev):
+    b, n = 96, 50
+    ref_env = TSPOracle(num_loc=n, seed=5)
+    td_ref = ref_env.reset(batch_size=[b])
+    env = TSPEnv(generator_params=dict(num_loc=n), seed=5, device=dev)
+    import rl4co_slap_amd as ra
+    from rl4co_slap_amd import _native as nat
+
+    td = env.reset(ra.TensorDict({"locs": td_ref["locs"].clone()}, [b]))
+    for t in range(n):
+        a_ref = tsp_nearest_action(td_ref)
+        out = torch.empty(b, dtype=torch.int64, device=dev)
+        nat.call("co_tsp_nearest_action", b, n, nat.ptr(td["locs"]), nat.ptr(td["action_mask"]),
+                 nat.ptr(td["current_node"]), int(t == 0), nat.ptr(out), nat.stream_of(out))
+        assert torch.equal(out.cpu(), a_ref), t
+        td_ref["action"] = a_ref
+        td_ref = ref_env.step(td_ref)["next"]
+        td["action"] = out
+        td = env.step(td)["next"]
+
+
+def _cvrp_pair(b, n, seed, dev):
+    import rl4co_slap_amd as ra
+
+    ref_env = CVRPOracle(num_loc=n, seed=seed)
+    gen = ref_env.generate([b])
+    td_ref = ref_env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    env = CVRPEnv(generator_params=dict(num_loc=n), seed=seed, device=dev)
+    td = env.reset(ra.TensorDict({k: v.clone() for k, v in gen.items()}, [b]))
+    return ref_env, td_ref, env, td
+
+
+CVRP_KEYS = ("locs", "action_mask", "current_node", "used_capacity", "vehicle_capacity", "visited")
+
+
+@pytest.mark.parametrize("b,n", [(1, 10), (64, 20), (33, 50), (128, 100)])
+def test_cvrp_random_feasible_episode(dev, b, n):
+    ref_env, td_ref, env, td = _cvrp_pair(b, n, 1234, dev)
+    for k in CVRP_KEYS:
+        assert_same(td[k], td_ref[k], k)
+    g = torch.Generator().manual_seed(11)
+    acts = []
+    t = 0
+    while not td_ref["done"].all():
+        a = torch.multinomial(td_ref["action_mask"].float(), 1, generator=g).squeeze(-1)
+        acts.append(a)
+        td_ref["action"] = a
+        td_ref = ref_env.step(td_ref)["next"]
+        td["action"] = a.to(dev)
+        td = env.step(td)["next"]
+        for k in CVRP_KEYS + ("done", "reward"):
+            assert_same(td[k], td_ref[k], f"{k}@{t}")
+        t += 1
+    acts = torch.stack(acts, 1)
+    assert_reward_close(env.get_reward(td, acts.to(dev)), ref_env.get_reward(td_ref, acts))
+
+
+def test_cvrp_nearest_policy_and_mask(dev):
+    from rl4co_slap_amd import _native as nat
+
+    b, n = 80, 30
+    ref_env, td_ref, env, td = _cvrp_pair(b, n, 77, dev)
+    acts = []
+    while not td_ref["done"].all():
+        a_ref = cvrp_nearest_action(td_ref)
+        cur = td["current_node"].contiguous()
+        out = torch.empty(b, dtype=torch.int64, device=dev)
+        nat.call("co_cvrp_nearest_action", b, n, nat.ptr(td["locs"]), nat.ptr(td["action_mask"]),
+                 nat.ptr(cur), nat.ptr(out), nat.stream_of(out))
+        assert torch.equal(out.cpu(), a_ref)
+        acts.append(a_ref)
+        td_ref["action"] = a_ref
+        td_ref = ref_env.step(td_ref)["next"]
+        td["action"] = out
+        td = env.step(td)["next"]
+        assert torch.equal(CVRPEnv.get_action_mask(td).cpu(), td_ref["action_mask"])
+    acts = torch.stack(acts, 1)
+    assert_reward_close(env.get_reward(td, acts.to(dev)), ref_env.get_reward(td_ref, acts))
+
+
+def test_cvrp_validity_errors(dev):
+    import rl4co_slap_amd as ra
+
+    env = CVRPEnv(generator_params=dict(num_loc=2), device=dev)
+    td = ra.TensorDict({"locs": torch.tensor([[[0.0, 1.0], [1.0, 0.0]]]),
+                        "depot": torch.tensor([[0.0, 0.0]]), "demand": torch.tensor([[0.6, 0.6]]),
+                        "capacity": torch.tensor([[1.0]])}, [1])
+    td = env.reset(td)
+    with pytest.raises(AssertionError, match="Used more than capacity"):
+        env.get_reward(td, torch.tensor([[1, 2, 0]], device=dev))
+    with pytest.raises(AssertionError, match="Invalid tour"):
+        env.get_reward(td, torch.tensor([[1, 1, 0]], device=dev))
+    r1 = env.get_reward(td, torch.tensor([[1, 0, 2, 0]], device=dev))
+    r2 = env.get_reward(td, torch.tensor([[1, 0, 2, 0, 0, 0]], device=dev))
+    assert r1.item() == r2.item() == pytest.approx(-4.0)
+
+
+@pytest.mark.parametrize("b", [1, 32, 100])
+def test_slap_episode(dev, b):
+    import rl4co_slap_amd as ra
+
+    ref_env = SLAPOracle(seed=1234)
+    np.random.seed(1234)
+    gen = ref_env.generate([b])
+    td_ref = ref_env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    env = SLAPEnv(seed=1, device=dev)
+    td = env.reset(ra.TensorDict({k: v.clone() for k, v in gen.items()}, [b]))
+    keys = ("action_mask", "assignment", "to_choose", "i", "ratio", "reward", "done", "terminated")
+    for k in keys:
+        assert_same(td[k], td_ref[k], k)
+    g = torch.Generator().manual_seed(3)
+    for t in range(20):
+        if t % 2 == 0:
+            a = torch.multinomial(td_ref["action_mask"].float(), 1, generator=g).squeeze(-1)
+        else:
+            a = slap_closest_free_action(td_ref)
+            from rl4co_slap_amd import _native as nat
+
+            out = torch.empty(b, dtype=torch.int64, device=dev)
+            nat.call("co_slap_closest_free_action", b, 100, nat.ptr(td["depot_loc_dist"]),
+                     nat.ptr(td["action_mask"]), nat.ptr(out), nat.stream_of(out))
+            assert torch.equal(out.cpu(), a)
+        td_ref["action"] = a
+        td_ref = ref_env.step(td_ref)["next"]
+        td["action"] = a.to(dev)
+        td = env.step(td)["next"]
+        for k in ("action_mask", "assignment", "to_choose", "i", "reward", "done"):
+            assert_same(td[k], td_ref[k], f"{k}@{t}")
+    assert_reward_close(env.get_reward(td, None), ref_env.get_reward(td_ref, None))
+
+
+def test_slap_reward_partial_assignment_wraps(dev):
+    # unassigned products (-1) index the last location, like python indexing
+    import rl4co_slap_amd as ra
+
+    ref_env = SLAPOracle(seed=2)
+    np.random.seed(2)
+    gen = ref_env.generate([16])
+    td_ref = ref_env.reset(TD({k: v.clone() for k, v in gen.items()}, [16]))
+    env = SLAPEnv(seed=1, device=dev)
+    td = env.reset(ra.TensorDict({k: v.clone() for k, v in gen.items()}, [16]))
+    assign = torch.randint(-1, 100, (16, 20), dtype=torch.int32)
+    td_ref["assignment"] = assign
+    td["assignment"] = assign.to(dev)
+    assert_reward_close(env.get_reward(td, None), ref_env.get_reward(td_ref, None))
+
+
+def test_empty_batch(dev):
+    env = TSPEnv(generator_params=dict(num_loc=10), device=dev)
+    td = env.reset(batch_size=[0])
+    td["action"] = torch.zeros(0, dtype=torch.int64, device=dev)
+    td = env.step(td)["next"]
+    assert td["action_mask"].shape == (0, 10)

@@ -1,0 +1,133 @@
+"""GPU parity for gather_by_index and the fused decode step (through the C ABI)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import decoding as odec
+from oracle.ops import gather_by_index as ref_gather
+from rl4co_slap_amd.utils.decoding import decode_step
+from rl4co_slap_amd.utils.ops import gather_by_index, get_tour_length, unbatchify_and_gather
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape,idx_shape,dtype", [
+    ((64, 100, 2), (64, 100), torch.float32),   # locs by actions (rewards)
+    ((33, 20), (33, 1), torch.float32),         # CVRP demand, squeeze=False case
+    ((17, 21, 128), (17,), torch.float32),      # context embedding by current_node
+    ((9, 7), (9,), torch.float32),              # logprob gather
+    ((5, 11, 3), (5, 4), torch.int64),
+    ((6, 13, 3), (6, 2), torch.bool),           # odd inner size -> byte path
+])
+def test_gather_matches_torch(dev, shape, idx_shape, dtype):
+    g = torch.Generator().manual_seed(0)
+    src = (torch.rand(shape, generator=g) * 100).to(dtype)
+    idx = torch.randint(0, shape[1], idx_shape, generator=g)
+    for squeeze in (True, False):
+        ref = ref_gather(src, idx, squeeze=squeeze)
+        out = gather_by_index(src.to(dev), idx.to(dev), squeeze=squeeze)
+        assert out.shape == ref.shape
+        assert torch.equal(out.cpu(), ref)
+
+
+def test_gather_strided_unbatchify(dev):
+    # POMO best actions: unbatchify (non-contiguous permuted view) then gather
+    s, b, t = 5, 7, 9
+    x = torch.randint(0, 100, (s * b, t))
+    m = torch.randint(0, s, (b,))
+    from oracle.ops import unbatchify_and_gather as ref_ubg
+
+    assert torch.equal(unbatchify_and_gather(x.to(dev), m.to(dev), s).cpu(), ref_ubg(x, m, s))
+
+
+def test_tour_length(dev):
+    locs = torch.rand(50, 13, 2)
+    from oracle.ops import get_tour_length as ref_tl
+
+    r = get_tour_length(locs.to(dev)).cpu()
+    assert torch.allclose(r, ref_tl(locs), rtol=1e-5, atol=1e-6)
+
+
+def _rand_mask(b, n, g):
+    m = torch.rand(b, n, generator=g) > 0.3
+    m[torch.arange(b), torch.randint(0, n, (b,), generator=g)] = True
+    return m
+
+
+@pytest.mark.parametrize("n", [20, 64, 100, 129, 500])
+@pytest.mark.parametrize("clip", [0.0, 10.0])
+def test_decode_greedy_and_evaluate(dev, n, clip):
+    g = torch.Generator().manual_seed(n)
+    b = 300
+    logits = torch.randn(b, n, generator=g) * 3
+    mask = _rand_mask(b, n, g)
+    # reference math on the clipped logits computed by the same path as the kernel input
+    lp_ref = odec.process_logits(logits.clone(), mask, 1.0, clip)
+    act, lp, full = decode_step(logits.to(dev), mask.to(dev), "greedy", tanh_clipping=clip,
+                                return_full=True)
+    full = full.cpu()
+    fin = torch.isfinite(lp_ref)
+    assert torch.equal(fin, torch.isfinite(full))
+    tol = 2e-6 if clip == 0 else 2e-5  # tanh: ocml vs the CPU vector tanh differ by ulps
+    assert (full[fin] - lp_ref[fin]).abs().max() <= tol
+    ref_act = odec.greedy(lp_ref, mask)
+    if clip == 0:
+        assert torch.equal(act.cpu(), ref_act)
+    else:  # equal wherever the top two are separated by more than the tanh ulp noise
+        top2 = lp_ref.topk(2, dim=-1).values
+        clear = (top2[:, 0] - top2[:, 1]) > 1e-4
+        assert torch.equal(act.cpu()[clear], ref_act[clear])
+    assert torch.allclose(lp.cpu(), full.gather(1, act.cpu()[:, None]).squeeze(1))
+    # evaluate: given actions
+    given = torch.multinomial(mask.float(), 1, generator=g).squeeze(1)
+    act_e, lp_e, _ = decode_step(logits.to(dev), mask.to(dev), "evaluate", tanh_clipping=clip,
+                                 action=given.to(dev))
+    assert torch.equal(act_e.cpu(), given)
+    ref_lp_e = lp_ref.gather(1, given[:, None]).squeeze(1)
+    assert (lp_e.cpu() - ref_lp_e).abs().max() <= tol
+
+
+def test_decode_greedy_exact_ties(dev):
+    # torch.argmax returns the first maximal index; ties built in logit space
+    b, n = 64, 100
+    logits = torch.zeros(b, n)
+    mask = torch.ones(b, n, dtype=torch.bool)
+    for r in range(b):
+        j = (r * 7) % n
+        logits[r, j] = 1.0
+        logits[r, (j + 13) % n] = 1.0
+        mask[r, : r % 5] = False
+    ref = odec.greedy(odec.process_logits(logits, mask), mask)
+    act, _, _ = decode_step(logits.to(dev), mask.to(dev), "greedy")
+    assert torch.equal(act.cpu(), ref)
+
+
+def test_decode_infeasible_flag(dev):
+    from rl4co_slap_amd import _native as nat
+
+    logits = torch.randn(4, 10)
+    mask = torch.zeros(4, 10, dtype=torch.bool)  # nothing feasible -> NaN logp, argmax 0
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    act, _, _ = decode_step(logits.to(dev), mask.to(dev), "greedy", status=st)
+    assert int(st.item()) & nat.ST_INFEASIBLE
+    ref_lp = odec.process_logits(logits, mask)
+    assert torch.equal(act.cpu(), ref_lp.argmax(-1))
+
+
+def test_decode_sampling_distribution(dev):
+    # statistical parity only (torch.multinomial's RNG stream is not reproduced)
+    b, n = 20000, 6
+    logits = torch.tensor([0.0, 1.0, 2.0, -1.0, 0.5, 3.0]).repeat(b, 1)
+    mask = torch.ones(b, n, dtype=torch.bool)
+    mask[:, 3] = False
+    act, lp, _ = decode_step(logits.to(dev), mask.to(dev), "sampling", seed=1234, offset=0)
+    act = act.cpu()
+    assert not (act == 3).any()
+    p = F.softmax(logits[0].masked_fill(~mask[0], float("-inf")), -1)
+    freq = torch.bincount(act, minlength=n).float() / b
+    assert (freq - p).abs().max() < 0.015
+    # deterministic given (seed, offset)
+    act2, _, _ = decode_step(logits.to(dev), mask.to(dev), "sampling", seed=1234, offset=0)
+    assert torch.equal(act, act2.cpu())
+    lp_ref = odec.process_logits(logits, mask).gather(1, act[:, None]).squeeze(1)
+    assert (lp.cpu() - lp_ref).abs().max() < 2e-6
