@@ -1,17 +1,21 @@
 """Env-steps/sec benchmark of the MI355X CO-env engine (BASELINE.json metric).
 
 ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
-``torch.distributed.run`` (one rank per GPU, RCCL).  A *step* of this benchmark is
-one full episode of the hot path over one batch resident in HBM: reset, every env
-step, and the episode-end reward (+ validity check).  Workload (BASELINE.json
-config 2): TSP-100, B = 65,536 instances per GPU (weak scaling), seeded synthetic
-instances ``manual_seed(1234); rand(B,100,2)`` and teacher-forced actions
-``manual_seed(4321); rand(B,100).argsort(1)`` (Evaluate-mode rollout).
+``torch.distributed.run`` (one rank per GPU; RCCL only for the timing reduction --
+the instance shards never exchange data).  A *step* of this benchmark is one full
+episode of the hot path over one batch resident in HBM: reset, every env step and
+the episode-end reward with the validity check.
 
-``value`` = env-steps/s over all ranks = world * B * N * K / max-over-ranks time.
-Rank 0 prints ONE JSON line.  ``cpu_baseline`` times the CPU oracle (the plain
-PyTorch restatement of the reference op sequence) on a bounded sample on this
-host; ``roofline`` prices the dominant kernel against HBM (8.0 TB/s).
+Headline workload (BASELINE.json config 2): TSP-100, B = 65,536 instances per GPU
+(weak scaling), ``manual_seed(1234 + rank); rand(B,100,2)``, teacher-forced actions
+``manual_seed(4321 + rank); rand(B,100).argsort(1)`` (Evaluate-mode rollout), run as
+the fused one-launch episode kernel ``co_tsp_rollout``.
+``value`` = world * B * 100 * K / (max over ranks of the timed wall time).
+
+Also reported (``modes``): the same episode stepwise (one launch per env step,
+TensorDict state in HBM between steps, HIP graph), the in-kernel nearest-unvisited
+policy, and SLAP (examples/slap.py instance, B = 16,384).  ``cpu_baseline`` is the
+CPU oracle (plain-PyTorch restatement of the reference op sequence) on this host.
 """
 from __future__ import annotations
 
@@ -27,18 +31,19 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--num-loc", type=int, default=100)
+    ap.add_argument("--slap-batch", type=int, default=16384)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--extra", action="store_true", help="also time SLAP / stepwise modes")
+    ap.add_argument("--no-modes", action="store_true", help="headline only")
     return ap.parse_args()
 
 
@@ -65,79 +70,109 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def tsp_inputs(b, n, rank, dev):
+def timed(run, steps, warmup, world, dev):
+    """W untimed runs, then exactly K timed runs bracketed by barrier + synchronize.
+    Returns (wall seconds, HIP-event seconds on the launching stream)."""
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    cur = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(cur)
+    for _ in range(steps):
+        run()
+    ev1.record(cur)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / 1e3
+
+
+def tsp_inputs(b, n, rank):
     torch.manual_seed(1234 + rank)
     locs = torch.rand(b, n, 2)
     torch.manual_seed(4321 + rank)
     acts = torch.rand(b, n).argsort(1)
-    return locs.to(dev), acts.to(dev)
+    return locs, acts
 
 
-def time_graph(ep, steps, warmup, world, dev, stream):
-    for _ in range(warmup):
-        ep.replay()
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    torch.cuda.synchronize(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
-        ep.replay()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    barrier(world)
-    torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
-    return wall, ev0.elapsed_time(ev1) / 1e3
+def cpu_threads():
+    # the box's CPU share (OMP_NUM_THREADS is set to it on the GPU pool), not the whole host
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
 
 
-def cpu_baseline_tsp(n, b_cpu=16384, episodes=3):
-    """The oracle (reference op sequence on CPU torch) timed on this host."""
+def cpu_baseline_tsp(locs, acts, episodes=3):
+    """The oracle (reference op sequence on CPU torch) on the same TSP workload."""
     from oracle.envs import TSPOracle
     from oracle.rollout import rollout
+    from oracle.td import TD
 
-    threads = os.cpu_count() or 1
+    threads = cpu_threads()
     torch.set_num_threads(threads)
+    b, n = acts.shape
     env = TSPOracle(num_loc=n, seed=1234)
-    torch.manual_seed(4321)
-    acts = torch.rand(b_cpu, n).argsort(1)
     times = []
-    for e in range(episodes + 1):
-        td = env.reset(batch_size=[b_cpu])
+    for _ in range(episodes + 1):
+        td = env.reset(TD({"locs": locs}, [b]))
         it = iter(range(n))
         t0 = time.perf_counter()
         rollout(env, td, lambda td: acts[:, next(it)])
         times.append(time.perf_counter() - t0)
-    times = sorted(times[1:])
-    med = times[len(times) // 2]
-    return {"value": b_cpu * n / med, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle TSP-{n} teacher-forced rollout (reset+{n} steps+reward), "
-                      f"B={b_cpu}, median of {episodes} episodes after 1 warm-up, "
+    med = sorted(times[1:])[len(times[1:]) // 2]
+    return {"value": b * n / med, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (CPU PyTorch restatement) TSP-{n} teacher-forced rollout: reset + "
+                      f"{n} x _step + get_reward with the double validity sort, B={b} (the full "
+                      f"GPU workload), median of {episodes} episodes after 1 warm-up, "
                       f"torch.set_num_threads({threads})"}
+
+
+def cpu_baseline_slap(b=2048, episodes=2):
+    import numpy as np
+
+    from oracle.envs import SLAPOracle, slap_closest_free_action
+    from oracle.rollout import rollout
+
+    torch.set_num_threads(cpu_threads())
+    env = SLAPOracle(seed=1234)
+    np.random.seed(1234)
+    gen = env.generate([b])
+    times = []
+    for _ in range(episodes + 1):
+        from oracle.td import TD
+
+        td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+        t0 = time.perf_counter()
+        rollout(env, td, slap_closest_free_action)
+        times.append(time.perf_counter() - t0)
+    med = sorted(times[1:])[len(times[1:]) // 2]
+    return {"value": b * 20 / med, "unit": "env-steps/s", "cores": cpu_threads(),
+            "sample": f"oracle SLAP rollout (closest-free policy, per-batch Python loop of "
+                      f"slap/env.py:61-62 kept), B={b}, median of {episodes}"}
 
 
 def main():
     args = parse()
     world, rank, dev = setup_dist()
     from rl4co_slap_amd import _native
-    from rl4co_slap_amd.rollout.engine import TSPStepwiseEpisode
+    from rl4co_slap_amd.rollout.engine import TSPFusedEpisode, TSPStepwiseEpisode
 
     _native.load()
     b, n = args.batch, args.num_loc
-    locs, acts = tsp_inputs(b, n, rank, dev)
-    ep = TSPStepwiseEpisode(locs, acts, policy="teacher", check=True).capture()
-    wall, gpu_s = time_graph(ep, args.steps, args.warmup, world, dev, ep.stream)
-    assert int(ep.status.item()) == 0, "invalid tour / index error in the benchmark episode"
+    locs_cpu, acts_cpu = tsp_inputs(b, n, rank)
+    locs, acts = locs_cpu.to(dev), acts_cpu.to(dev)
+
+    # ---- headline: fused one-launch episode, eager back-to-back launches ---------------
+    ep = TSPFusedEpisode(locs, acts, policy="teacher", check=True)
+    s = lambda: ep._launch(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
+    wall, ev = timed(s, args.steps, args.warmup, world, dev)
+    assert int(ep.status.item()) == 0, "invalid tour in the benchmark episode"
     t = max_over_ranks(wall, world, dev)
     value = world * b * n * args.steps / t
-
-    # dominant kernel: co_tsp_step; time a graph of N back-to-back steps with events
-    steps_only = _StepsOnly(ep)
-    steps_only.capture()
-    sw, sg = time_graph(steps_only, max(3, args.steps // 2), 2, world, dev, steps_only.stream)
-    per_launch = sg / (max(3, args.steps // 2) * n)
-    bytes_per_launch = (2 * n + 50) * b  # SURVEY.md 8d: 2N+50 B per TSP env-step
+    per_launch = ev / args.steps
+    bytes_per_launch = b * (17 * n + 30)  # DESIGN.md: co_tsp_rollout algorithmic bytes
     achieved = bytes_per_launch / per_launch / 1e9
 
     out = {
@@ -145,53 +180,65 @@ def main():
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": t / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8+i64+f32",
-        "data": "synthetic (seeded torch.rand instances, teacher-forced argsort actions)",
-        "config": {"workload": f"TSP-{n} teacher-forced episode (reset + {n} x step + reward), "
-                               f"stepwise HIP-graph", "batch_per_gpu": b, "num_loc": n,
-                   "parallelism": f"dp{world} (instance shards, no data-path collective)"},
-        "roofline": {"bound": "hbm", "kernel": "co_tsp_step (tsp_step_kernel)",
+        "data": "synthetic: seeded torch.rand TSP instances, teacher-forced argsort actions",
+        "config": {"workload": f"TSP-{n} B={b}/GPU teacher-forced episode (reset + {n} env steps + "
+                               "reward + validity) as one fused launch (co_tsp_rollout)",
+                   "batch_per_gpu": b, "num_loc": n, "env_steps_per_episode": n,
+                   "parallelism": f"dp{world}: disjoint instance shards, no data-path collective"},
+        "roofline": {"bound": "hbm", "kernel": "tsp_rollout_kernel<2,false> (co_tsp_rollout)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "per_launch_us": per_launch * 1e6,
-                     "note": "event time / launches of a graph of back-to-back step kernels "
-                             "(includes the launch boundary)"},
+                     "bytes_per_launch": bytes_per_launch, "launch_us": per_launch * 1e6},
     }
+
+    if not args.no_modes:
+        modes = {}
+        # stepwise: one launch per env step, TensorDict state in HBM (2N+50 B/step)
+        sw = TSPStepwiseEpisode(locs, acts, policy="teacher", check=True).capture()
+        k = max(3, args.steps // 5)
+        wall_s, ev_s = timed(sw.replay, k, 2, world, dev)
+        t_s = max_over_ranks(wall_s, world, dev)
+        modes["tsp_stepwise_graph"] = {
+            "value": world * b * n * k / t_s, "ms_per_episode": t_s / k * 1e3,
+            "bytes_per_env_step": 2 * n + 50,
+            "achieved_GBps_incl_reset_reward": b * n * (2 * n + 50) * k / ev_s / 1e9}
+        del sw
+        # in-kernel nearest-unvisited policy, fused
+        ne = TSPFusedEpisode(locs, None, policy="nearest", check=True)
+        sn = lambda: ne._launch(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
+        wall_n, ev_n = timed(sn, k, 1, world, dev)
+        t_n = max_over_ranks(wall_n, world, dev)
+        modes["tsp_fused_nearest"] = {"value": world * b * n * k / t_n,
+                                      "ms_per_episode": t_n / k * 1e3}
+        del ne
+        # SLAP (examples/slap.py instance), stepwise graph, closest-free policy
+        modes["slap_stepwise_graph"] = bench_slap(args.slap_batch, k, world, rank, dev)
+        out["modes"] = modes
+
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline_tsp(n)
+        out["cpu_baseline"] = cpu_baseline_tsp(locs_cpu, acts_cpu)
+        if not args.no_modes:
+            out["cpu_baseline_slap"] = cpu_baseline_slap()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-class _StepsOnly:
-    """A graph of the episode's N step launches only (for per-launch timing)."""
+def bench_slap(b, k, world, rank, dev):
+    import numpy as np
 
-    def __init__(self, ep):
-        self.ep = ep
-        self.stream = ep.stream
-        self.graph = None
+    from rl4co_slap_amd.envs.slap import SLAPGenerator
+    from rl4co_slap_amd.rollout.engine import SLAPStepwiseEpisode
 
-    def _launch(self, s):
-        from rl4co_slap_amd import _native as nat
-
-        ep = self.ep
-        b, n = ep.b, ep.n
-        for t in range(n):
-            src, dst = t & 1, (t + 1) & 1
-            nat.call("co_tsp_step", b, n, nat.ptr(ep.acts[t]), nat.ptr(ep.mask[src]),
-                     nat.ptr(ep.mask[dst]), nat.ptr(ep.i[src]), nat.ptr(ep.i[dst]),
-                     nat.ptr(ep.first[src]), nat.ptr(ep.first[dst]), nat.ptr(ep.cur),
-                     nat.ptr(ep.done), nat.ptr(ep.step_reward), 0, None, nat.ptr(ep.status), s)
-
-    def capture(self):
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=self.stream):
-            self._launch(torch.cuda.current_stream().cuda_stream)
-        self.graph = g
-
-    def replay(self):
-        self.graph.replay()
+    torch.manual_seed(1234 + rank)
+    np.random.seed(1234 + rank)
+    td = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
+    ep = SLAPStepwiseEpisode(td, policy="closest").capture()
+    wall, ev = timed(ep.replay, k, 2, world, dev)
+    t = max_over_ranks(wall, world, dev)
+    return {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3, "batch_per_gpu": b,
+            "bytes_per_env_step": 234}
 
 
 if __name__ == "__main__":

@@ -190,6 +190,23 @@ int co_cvrp_nearest_action(int64_t batch, int64_t num_loc, const float* locs,
 int co_slap_closest_free_action(int64_t batch, int64_t num_slots, const float* depot_loc_dist,
                                 const uint8_t* action_mask, int64_t* action_out, void* stream);
 
+/* -------------------------------------------- fused episode rollouts */
+
+/* One launch per episode (reset + N steps + reward) for the env-only rollout of
+ * rl4co/utils/decoding.py:88-109 with the policy in-kernel.  Each step applies
+ * TSPEnv._step (tsp/env.py:67-93) to register state; only what a caller can
+ * observe after rollout() is written: the final action_mask[B,N], first_node[B],
+ * current_node[B], i[B,1] (= N), done[B], the last step's bool reward[B], the
+ * episode reward[B] (= -closed tour length, TSPEnv.get_reward) and, for the
+ * in-kernel policy, the actions.  Actions are step-major [N, B] (row t = the [B]
+ * action tensor of step t).  acts_in != NULL: teacher-forced (Evaluate mode);
+ * acts_in == NULL: nearest-unvisited policy (co_tsp_nearest_action) writing
+ * acts_out.  check != 0: a non-permutation sets CO_ST_INVALID_TOUR.  N <= 256. */
+int co_tsp_rollout(int64_t batch, int64_t num_loc, const float* locs, const int64_t* acts_in,
+                   int64_t* acts_out, uint8_t* action_mask, int64_t* first_node,
+                   int64_t* current_node, int64_t* i, uint8_t* done, uint8_t* step_reward,
+                   float* reward, int check, int32_t* status, void* stream);
+
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 

@@ -41,6 +41,7 @@ _SIGS = {
     "co_cvrp_nearest_action": [_i64, _i64, _p, _p, _p, _p, _p],
     "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],
     "co_count_not_done": [_p, _i64, _p, _p],
+    "co_tsp_rollout": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
 }
 
 ST_INVALID_TOUR = 1

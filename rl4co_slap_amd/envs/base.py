@@ -67,8 +67,9 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         if seed is None:
             seed = torch.empty((), dtype=torch.int64).random_().item()
         self.set_seed(seed)
-        # host-side knowledge of td["i"] tensors this env produced: tensor -> (version, value)
-        self._i_known = weakref.WeakKeyDictionary()
+        # host-side knowledge of td["i"] tensors this env produced:
+        # id(tensor) -> (weakref, version, uniform value)
+        self._i_known = {}
 
     # -- seeding (base.py:288-291) ---------------------------------------------
     def set_seed(self, seed: Optional[int]):
@@ -177,10 +178,12 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
 
     # -- i-tracking for the batch-wide `i.all() == 0` test ------------------------
     def _remember_i(self, t: torch.Tensor, value: int):
-        self._i_known[t] = (t._version, value)
+        if len(self._i_known) > 64:  # drop entries whose tensors are gone
+            self._i_known = {k: v for k, v in self._i_known.items() if v[0]() is not None}
+        self._i_known[id(t)] = (weakref.ref(t), t._version, value)
 
     def _known_i(self, t: torch.Tensor):
-        rec = self._i_known.get(t)
-        if rec is None or rec[0] != t._version:
+        rec = self._i_known.get(id(t))
+        if rec is None or rec[0]() is not t or rec[1] != t._version:
             return None
-        return rec[1]
+        return rec[2]

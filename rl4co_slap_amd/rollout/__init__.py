@@ -1,3 +1,3 @@
-from .engine import SLAPStepwiseEpisode, TSPStepwiseEpisode
+from .engine import SLAPStepwiseEpisode, TSPFusedEpisode, TSPStepwiseEpisode
 
-__all__ = ["TSPStepwiseEpisode", "SLAPStepwiseEpisode"]
+__all__ = ["TSPStepwiseEpisode", "TSPFusedEpisode", "SLAPStepwiseEpisode"]

@@ -154,3 +154,43 @@ class SLAPStepwiseEpisode(_GraphEpisode):
         k = self.p & 1
         return {"action_mask": self.mask[k], "i": self.i[k], "assignment": self.assign,
                 "done": self.done, "reward": self.reward, "actions": self.acts.t()}
+
+
+class TSPFusedEpisode(_GraphEpisode):
+    """The whole TSP episode as ONE launch (``co_tsp_rollout``): reset, N steps with the
+    policy in-kernel (teacher-forced step-major actions, or nearest-unvisited) and the
+    reward, state in registers/LDS; writes the post-rollout TensorDict columns."""
+
+    def __init__(self, locs: torch.Tensor, actions: torch.Tensor = None, policy: str = "teacher",
+                 check: bool = True):
+        super().__init__(locs.device)
+        b, n, _ = locs.shape
+        d = locs.device
+        self.b, self.n, self.policy, self.check = b, n, policy, check
+        self.locs = locs.contiguous()
+        if policy == "teacher":
+            assert actions is not None and actions.shape == (b, n)
+            self.acts = actions.t().contiguous()
+        else:
+            self.acts = torch.empty((n, b), dtype=torch.int64, device=d)
+        self.mask = torch.empty((b, n), dtype=torch.bool, device=d)
+        self.first = torch.empty(b, dtype=torch.int64, device=d)
+        self.cur = torch.empty(b, dtype=torch.int64, device=d)
+        self.i = torch.empty((b, 1), dtype=torch.int64, device=d)
+        self.done = torch.empty(b, dtype=torch.bool, device=d)
+        self.step_reward = torch.empty(b, dtype=torch.bool, device=d)
+        self.reward = torch.empty(b, dtype=torch.float32, device=d)
+        self.status = torch.zeros(1, dtype=torch.int32, device=d)
+
+    def _launch(self, s):
+        teacher = self.policy == "teacher"
+        nat.call("co_tsp_rollout", self.b, self.n, nat.ptr(self.locs),
+                 nat.ptr(self.acts) if teacher else None, None if teacher else nat.ptr(self.acts),
+                 nat.ptr(self.mask), nat.ptr(self.first), nat.ptr(self.cur), nat.ptr(self.i),
+                 nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.reward),
+                 int(self.check), nat.ptr(self.status), s)
+
+    def final_state(self):
+        return {"action_mask": self.mask, "i": self.i, "first_node": self.first,
+                "current_node": self.cur, "done": self.done, "reward": self.reward,
+                "actions": self.acts.t()}

@@ -1,0 +1,91 @@
+"""GPU parity for the rollout engine (stepwise HIP-graph and the fused one-launch
+episode) against the oracle's env-only rollout (rl4co/utils/decoding.py:88-109)."""
+import pytest
+import torch
+
+from oracle.envs import TSPOracle, tsp_nearest_action
+from oracle.rollout import rollout as ref_rollout
+from rl4co_slap_amd.rollout.engine import TSPFusedEpisode, TSPStepwiseEpisode
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(b, n, seed, policy):
+    env = TSPOracle(num_loc=n, seed=seed)
+    td = env.reset(batch_size=[b])
+    locs = td["locs"].clone()
+    if policy == "teacher":
+        acts = torch.rand(b, n, generator=torch.Generator().manual_seed(seed + 1)).argsort(1)
+        it = iter(range(n))
+        r, tdf, a = ref_rollout(env, td, lambda t: acts[:, next(it)])
+    else:
+        r, tdf, a = ref_rollout(env, td, tsp_nearest_action)
+    return locs, a, r, tdf
+
+
+def _check(state, a, r, tdf, exact_reward=False):
+    assert torch.equal(state["action_mask"].cpu(), tdf["action_mask"])
+    assert torch.equal(state["first_node"].cpu(), tdf["first_node"])
+    assert torch.equal(state["current_node"].cpu(), tdf["current_node"])
+    assert torch.equal(state["i"].cpu(), tdf["i"])
+    assert torch.equal(state["done"].cpu(), tdf["done"])
+    assert torch.equal(state["actions"].cpu(), a)
+    got = state["reward"].cpu()
+    assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
+
+
+@pytest.mark.parametrize("cls", [TSPFusedEpisode, TSPStepwiseEpisode])
+@pytest.mark.parametrize("b,n", [(1, 5), (100, 20), (256, 100), (77, 64), (65, 65), (40, 150)])
+@pytest.mark.parametrize("policy", ["teacher", "nearest"])
+def test_tsp_rollout_matches_oracle(dev, cls, b, n, policy):
+    locs, a, r, tdf = _ref(b, n, 1234 + n, policy)
+    ep = cls(locs.to(dev), a.to(dev) if policy == "teacher" else None, policy=policy)
+    ep.run_eager()
+    torch.cuda.synchronize()
+    assert int(ep.status.item()) == 0
+    _check(ep.final_state(), a, r, tdf)
+    # graph replay gives the same result
+    ep.capture()
+    ep.replay()
+    torch.cuda.synchronize()
+    _check(ep.final_state(), a, r, tdf)
+
+
+def test_tsp_fused_invalid_tour_flag(dev):
+    b, n = 70, 12
+    locs = torch.rand(b, n, 2)
+    acts = torch.arange(n).repeat(b, 1)
+    acts[33, 5] = 7  # duplicate -> not a permutation
+    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep.run_eager()
+    torch.cuda.synchronize()
+    assert int(ep.status.item()) & 1
+
+
+def test_tsp_fused_full_size_properties(dev):
+    # BASELINE config 2 size: size-independent properties (oracle too slow to mirror whole)
+    b, n = 65536, 100
+    g = torch.Generator().manual_seed(1234)
+    locs = torch.rand(b, n, 2, generator=g)
+    acts = torch.rand(b, n, generator=torch.Generator().manual_seed(4321)).argsort(1)
+    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep.run_eager()
+    torch.cuda.synchronize()
+    st = ep.final_state()
+    assert int(ep.status.item()) == 0
+    assert not st["action_mask"].any() and st["done"].all()
+    assert (st["i"] == n).all()
+    assert torch.equal(st["first_node"].cpu(), acts[:, 0])
+    assert torch.equal(st["current_node"].cpu(), acts[:, -1])
+    # spot-check 512 random instances against the oracle reward
+    idx = torch.randperm(b, generator=g)[:512]
+    from oracle.ops import gather_by_index, get_tour_length
+
+    ref = -get_tour_length(gather_by_index(locs[idx], acts[idx]))
+    got = st["reward"].cpu()[idx]
+    assert ((got - ref).abs() <= 1e-5 * ref.abs().clamp(min=1)).all()
+    # rotation invariance of the closed tour length
+    ep2 = TSPFusedEpisode(locs.to(dev), acts.roll(37, dims=1).to(dev))
+    ep2.run_eager()
+    torch.cuda.synchronize()
+    assert ((ep2.reward - ep.reward).abs() <= 1e-5 * ep.reward.abs()).all()
