@@ -207,6 +207,19 @@ int co_tsp_rollout(int64_t batch, int64_t num_loc, const float* locs, const int6
                    int64_t* current_node, int64_t* i, uint8_t* done, uint8_t* step_reward,
                    float* reward, int check, int32_t* status, void* stream);
 
+/* SLAP episode in one launch (slap/env.py:38-143): P steps (product t <- the
+ * step-t location; locations masked; done at i == P-1) then the per-order pick
+ * tour reward.  Writes action_mask[B,L], assignment[B,P] (from assign_in, the
+ * generator's -1s), i[B,1] (= P), done[B,1], step_reward[B,1], reward[B] and
+ * ratio[B,L] = 0 (nullable).  acts_in != NULL: teacher-forced step-major [P,B];
+ * acts_in == NULL: closest-free policy on depot_dist, written to acts_out.  L <= 256. */
+int co_slap_rollout(int64_t batch, int64_t num_slots, int64_t n_products, int64_t n_orders,
+                    int64_t order_size, const float* locs, const int64_t* picklist,
+                    const float* depot_dist, const int32_t* assign_in, const int64_t* acts_in,
+                    int64_t* acts_out, uint8_t* action_mask, int32_t* assignment, int64_t* i,
+                    uint8_t* done, uint8_t* step_reward, float* reward, float* ratio,
+                    int32_t* status, void* stream);
+
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 

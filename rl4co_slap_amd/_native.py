@@ -42,6 +42,8 @@ _SIGS = {
     "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],
     "co_count_not_done": [_p, _i64, _p, _p],
     "co_tsp_rollout": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
+    "co_slap_rollout": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                        _p, _p, _p, _p],
 }
 
 ST_INVALID_TOUR = 1

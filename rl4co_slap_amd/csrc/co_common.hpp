@@ -83,3 +83,8 @@ inline int launch_status() {
 }
 
 }  // namespace co
+
+// internal (not part of the public C ABI): rollout.hip's thread-per-instance reward
+int co_internal_tsp_reward_stepmajor(int64_t B, int64_t N, const float* locs,
+                                     const int64_t* acts, int64_t st, int check, float* reward,
+                                     int32_t* status, void* stream);

@@ -43,17 +43,21 @@ struct SlapRowEpilogue {
   uint8_t* done;
   uint8_t* reward;
   int32_t* status;
-  __device__ void operator()(int64_t b, int64_t action, int) const {
-    int64_t p = (int64_t)(int)to_choose[b * tc_stride];  // .to(torch.int), env.py:52
+  struct Row {
+    int64_t i;
+    float product;
+  };
+  __device__ Row load(int64_t b) const { return {i_in[b], to_choose[b * tc_stride]}; }
+  __device__ void store(int64_t b, int64_t action, int, const Row& r) const {
+    int64_t p = (int64_t)(int)r.product;  // .to(torch.int), env.py:52
     if (p < 0) p += P;
     if (p < 0 || p >= P) {
       set_status(status, CO_ST_INDEX_RANGE);
     } else {
       assign_out[b * P + p] = (int32_t)action;  // .to(torch.int), env.py:53-54
     }
-    const int64_t iv = i_in[b];
-    done[b] = iv == (int64_t)(P - 1);
-    i_out[b] = iv + 1;
+    done[b] = r.i == (int64_t)(P - 1);
+    i_out[b] = r.i + 1;
     reward[b] = 0;
   }
 };
@@ -70,7 +74,8 @@ __global__ __launch_bounds__(256) void slap_step_kernel(int64_t B, int L, const 
     const int32_t* s = assign_in + row0 * epi.P;
     int32_t* d = epi.assign_out + row0 * epi.P;
     for (int64_t k = threadIdx.x; k < n; k += kTileThreads) d[k] = s[k];
-    // the epilogue's element write (after the tile's __syncthreads) orders after this copy
+    // the epilogue's element write must follow every thread's copy of the block
+    __syncthreads();
   }
   mask_clear_tile<false, true>(B, L, action, mask_in, mask_out, epi.status, vec != 0, epi);
 }

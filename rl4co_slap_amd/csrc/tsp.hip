@@ -46,11 +46,13 @@ struct TspRowEpilogue {
   uint8_t* done;
   uint8_t* reward;
   int take_first;
-  __device__ void operator()(int64_t b, int64_t action, int remaining) const {
-    const int64_t f = take_first ? action : first_in[b];
-    const int64_t iv = i_in[b];
-    first_out[b] = f;
-    i_out[b] = iv + 1;
+  struct Row {
+    int64_t i, first;
+  };
+  __device__ Row load(int64_t b) const { return {i_in[b], take_first ? 0 : first_in[b]}; }
+  __device__ void store(int64_t b, int64_t action, int remaining, const Row& r) const {
+    first_out[b] = take_first ? action : r.first;
+    i_out[b] = r.i + 1;
     if (cur_out) cur_out[b] = action;
     done[b] = remaining == 0;
     reward[b] = 0;
@@ -184,6 +186,12 @@ extern "C" int co_tsp_reward(int64_t B, int64_t N, int64_t T, const float* locs,
   if (B == 0) return CO_OK;
   if (!locs || !actions || !reward || (check && !status)) return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  // step-major actions ([T, B], the stepwise engine's layout): thread per instance,
+  // coalesced [B]-row loads, LDS-staged coordinates (rollout.hip)
+  if (sb == 1 && st == B && T == N && N <= 256 && B > 1 &&
+      (reinterpret_cast<uintptr_t>(locs) & 15) == 0)
+    return co_internal_tsp_reward_stepmajor(B, N, locs, actions, st, check, reward, status,
+                                            stream);
   const size_t words = (size_t)((T + 31) / 32);
   constexpr int W = 4;
   const size_t shmem = check ? W * words * sizeof(uint32_t) : 0;

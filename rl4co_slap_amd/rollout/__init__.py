@@ -1,3 +1,3 @@
-from .engine import SLAPStepwiseEpisode, TSPFusedEpisode, TSPStepwiseEpisode
+from .engine import SLAPFusedEpisode, SLAPStepwiseEpisode, TSPFusedEpisode, TSPStepwiseEpisode
 
-__all__ = ["TSPStepwiseEpisode", "TSPFusedEpisode", "SLAPStepwiseEpisode"]
+__all__ = ["TSPStepwiseEpisode", "TSPFusedEpisode", "SLAPStepwiseEpisode", "SLAPFusedEpisode"]

@@ -194,3 +194,47 @@ class TSPFusedEpisode(_GraphEpisode):
         return {"action_mask": self.mask, "i": self.i, "first_node": self.first,
                 "current_node": self.cur, "done": self.done, "reward": self.reward,
                 "actions": self.acts.t()}
+
+
+class SLAPFusedEpisode(_GraphEpisode):
+    """The whole SLAP episode as ONE launch (``co_slap_rollout``): reset, P steps with
+    teacher-forced step-major actions or the closest-free policy, and the pick-tour
+    reward; writes the post-rollout TensorDict columns."""
+
+    def __init__(self, td, actions=None, policy: str = "teacher", write_ratio: bool = True):
+        locs = td["locs"]
+        super().__init__(locs.device)
+        d = locs.device
+        b, l = locs.shape[0], locs.shape[1]
+        p = td["freq"].shape[-2]
+        self.b, self.l, self.p, self.policy = b, l, p, policy
+        self.locs = locs.contiguous()
+        self.picklist = td["picklist"].contiguous()
+        self.o, self.k = self.picklist.shape[1], self.picklist.shape[2]
+        self.depot_dist = td["depot_loc_dist"].contiguous()
+        self.assign0 = td["assignment"].contiguous()
+        if policy == "teacher":
+            self.acts = actions.t().contiguous()
+        else:
+            self.acts = torch.empty((p, b), dtype=torch.int64, device=d)
+        self.mask = torch.empty((b, l), dtype=torch.bool, device=d)
+        self.assign = torch.empty_like(self.assign0)
+        self.i = torch.empty((b, 1), dtype=torch.int64, device=d)
+        self.done = torch.empty((b, 1), dtype=torch.bool, device=d)
+        self.step_reward = torch.empty((b, 1), dtype=torch.bool, device=d)
+        self.reward = torch.empty(b, dtype=torch.float32, device=d)
+        self.ratio = torch.empty((b, l), dtype=torch.float32, device=d) if write_ratio else None
+        self.status = torch.zeros(1, dtype=torch.int32, device=d)
+
+    def _launch(self, s):
+        teacher = self.policy == "teacher"
+        nat.call("co_slap_rollout", self.b, self.l, self.p, self.o, self.k, nat.ptr(self.locs),
+                 nat.ptr(self.picklist), nat.ptr(self.depot_dist), nat.ptr(self.assign0),
+                 nat.ptr(self.acts) if teacher else None, None if teacher else nat.ptr(self.acts),
+                 nat.ptr(self.mask), nat.ptr(self.assign), nat.ptr(self.i), nat.ptr(self.done),
+                 nat.ptr(self.step_reward), nat.ptr(self.reward), nat.ptr(self.ratio),
+                 nat.ptr(self.status), s)
+
+    def final_state(self):
+        return {"action_mask": self.mask, "i": self.i, "assignment": self.assign,
+                "done": self.done, "reward": self.reward, "actions": self.acts.t()}

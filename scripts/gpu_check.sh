@@ -9,3 +9,7 @@ step timeout -k 10 300 python __graft_entry__.py > gpurun_out/smoke.log 2>&1
 tail -3 gpurun_out/smoke.log
 step timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1
 tail -3 gpurun_out/bench.log
+if [ -n "$WITH_PROF" ]; then
+  step bash scripts/gpu_prof.sh
+  cat gpurun_out/prof/run_kernel_stats.csv | cut -c1-200
+fi

@@ -89,3 +89,44 @@ def test_tsp_fused_full_size_properties(dev):
     ep2.run_eager()
     torch.cuda.synchronize()
     assert ((ep2.reward - ep.reward).abs() <= 1e-5 * ep.reward.abs()).all()
+
+
+def _slap_ref(b, seed, policy):
+    import numpy as np
+
+    from oracle.envs import SLAPOracle, slap_closest_free_action
+    from oracle.td import TD
+
+    env = SLAPOracle(seed=seed)
+    np.random.seed(seed)
+    gen = env.generate([b])
+    td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    if policy == "teacher":
+        g = torch.Generator().manual_seed(seed)
+        acts = torch.stack([torch.randperm(99, generator=g)[:20] + 1 for _ in range(b)])
+        it = iter(range(20))
+        r, tdf, a = ref_rollout(env, td, lambda t: acts[:, next(it)])
+    else:
+        r, tdf, a = ref_rollout(env, td, slap_closest_free_action)
+    return gen, a, r, tdf
+
+
+@pytest.mark.parametrize("cls_name", ["SLAPFusedEpisode", "SLAPStepwiseEpisode"])
+@pytest.mark.parametrize("b", [1, 64, 100, 300])
+@pytest.mark.parametrize("policy", ["teacher", "closest"])
+def test_slap_rollout_matches_oracle(dev, cls_name, b, policy):
+    import rl4co_slap_amd.rollout.engine as eng
+    from rl4co_slap_amd.td import TensorDict
+
+    gen, a, r, tdf = _slap_ref(b, 1234 + b, policy)
+    td = TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev)
+    ep = getattr(eng, cls_name)(td, a.to(dev) if policy == "teacher" else None, policy=policy)
+    ep.run_eager()
+    torch.cuda.synchronize()
+    assert int(ep.status.item()) == 0
+    st = ep.final_state()
+    for k in ("action_mask", "i", "assignment", "done"):
+        assert torch.equal(st[k].cpu(), tdf[k]), k
+    assert torch.equal(st["actions"].cpu(), a)
+    got = st["reward"].cpu()
+    assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
