@@ -153,6 +153,23 @@ def cpu_baseline_slap(b=2048, episodes=2):
                       f"slap/env.py:61-62 kept), B={b}, median of {episodes}"}
 
 
+def pmc_traffic(target, kernel_prefix):
+    """HBM bytes per launch measured by rocprofv3 PMC passes (scripts/gpu_pmc.sh ->
+    tools/pmc_summarize.py -> profiles/*_pmc_traffic.json, newest round first)."""
+    import glob
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), reverse=True):
+        try:
+            data = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for e in data.get("kernels", {}).values():
+            if e.get("target") == target and e.get("kernel", "").startswith(kernel_prefix) \
+                    and "hbm_bytes_per_launch" in e:
+                return e["hbm_bytes_per_launch"], os.path.basename(f)
+    return None, None
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist()
@@ -174,6 +191,9 @@ def main():
     per_launch = ev / args.steps
     bytes_per_launch = b * (17 * n + 30)  # co_tsp_rollout algorithmic bytes
     achieved = bytes_per_launch / per_launch / 1e9
+    traffic, traffic_src = (None, None)
+    if (b, n) == (65536, 100):
+        traffic, traffic_src = pmc_traffic("tsp_fused_teacher", "tsp_rollout_kernel<2, false, true>")
 
     out = {
         "metric": "env-steps/sec (batch×decode) SLAP & TSP-100 at 1/2/4/8 MI355X",
@@ -187,7 +207,8 @@ def main():
                    "parallelism": f"dp{world}: disjoint instance shards, no data-path collective"},
         "roofline": {"bound": "hbm", "kernel": "tsp_rollout_kernel<2,false> (co_tsp_rollout)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "launch_us": per_launch * 1e6},
     }
 
@@ -211,8 +232,8 @@ def main():
         modes["tsp_fused_nearest"] = {"value": world * b * n * k / t_n,
                                       "ms_per_episode": t_n / k * 1e3}
         del ne
-        # SLAP (examples/slap.py instance), stepwise graph, closest-free policy
-        modes["slap_stepwise_graph"] = bench_slap(args.slap_batch, k, world, rank, dev)
+        # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
+        modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
         out["modes"] = modes
 
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -233,12 +254,24 @@ def bench_slap(b, k, world, rank, dev):
 
     torch.manual_seed(1234 + rank)
     np.random.seed(1234 + rank)
+    from rl4co_slap_amd.rollout.engine import SLAPFusedEpisode
+
     td = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
+    out = {}
+    fu = SLAPFusedEpisode(td, policy="closest")
+    run = lambda: fu._launch(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
+    wall, ev = timed(run, 4 * k, 2, world, dev)
+    assert int(fu.status.item()) == 0
+    t = max_over_ranks(wall, world, dev)
+    out["slap_fused_closest"] = {"value": world * b * 20 * 4 * k / t,
+                                 "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
+                                 "launch_us": ev / (4 * k) * 1e6}
     ep = SLAPStepwiseEpisode(td, policy="closest").capture()
     wall, ev = timed(ep.replay, k, 2, world, dev)
     t = max_over_ranks(wall, world, dev)
-    return {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3, "batch_per_gpu": b,
-            "bytes_per_env_step": 234}
+    out["slap_stepwise_graph"] = {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3,
+                                  "batch_per_gpu": b, "bytes_per_env_step": 234}
+    return out
 
 
 if __name__ == "__main__":

@@ -1,0 +1,43 @@
+"""Small driver for PMC passes: launches one engine kernel K times on the bench workload
+(diagnostic tool, not part of the product)."""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--kernel", default="tsp_fused_teacher")
+ap.add_argument("--k", type=int, default=5)
+args = ap.parse_args()
+dev = torch.device("cuda:0")
+from rl4co_slap_amd import _native  # noqa: E402
+from rl4co_slap_amd.rollout import engine  # noqa: E402
+
+_native.load()
+if args.kernel.startswith("tsp"):
+    torch.manual_seed(1234)
+    locs = torch.rand(65536, 100, 2)
+    torch.manual_seed(4321)
+    acts = torch.rand(65536, 100).argsort(1)
+    if args.kernel == "tsp_fused_teacher":
+        ep = engine.TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    elif args.kernel == "tsp_fused_nearest":
+        ep = engine.TSPFusedEpisode(locs.to(dev), None, policy="nearest")
+    else:
+        ep = engine.TSPStepwiseEpisode(locs.to(dev), acts.to(dev))
+else:
+    import numpy as np
+
+    from rl4co_slap_amd.envs.slap import SLAPGenerator
+
+    torch.manual_seed(1234)
+    np.random.seed(1234)
+    td = SLAPGenerator(materialize_dist_mat=False)(16384).to(dev)
+    ep = engine.SLAPFusedEpisode(td, None, policy="closest")
+for _ in range(args.k):
+    ep.run_eager()
+torch.cuda.synchronize()
+print("ok", args.kernel)
