@@ -234,6 +234,9 @@ def main():
         del ne
         # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
         modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
+        # POMO TSP-100 (config 5): 1,024 instances x 100 starts per GPU, decode-fused steps
+        # on HBM-resident logits, shared baseline + RCCL all-gather of per-instance results
+        modes["pomo_tsp100"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev)
         out["modes"] = modes
 
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -272,6 +275,33 @@ def bench_slap(b, k, world, rank, dev):
     out["slap_stepwise_graph"] = {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "bytes_per_env_step": 234}
     return out
+
+
+def bench_pomo(b, n, k, world, rank, dev):
+    from rl4co_slap_amd.rollout.pomo import POMOEpisode, global_metrics
+
+    torch.manual_seed(1234 + rank)
+    locs = torch.rand(b, n, 2).to(dev)
+    e = b * n
+    g = torch.Generator(device=dev).manual_seed(99 + rank)
+    logits = torch.randn((n - 1, e, n), generator=g, device=dev)  # policy-network stand-in
+    ep = POMOEpisode(locs, logits, tanh_clipping=10.0).capture()
+
+    def run():
+        ep.replay()
+
+    wall, ev = timed(run, k, 1, world, dev)
+    assert int(ep.status.item()) == 0
+    t = max_over_ranks(wall, world, dev)
+    t0 = time.perf_counter()
+    m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n)  # the RCCL exchange
+    torch.cuda.synchronize(dev)
+    t_ag = time.perf_counter() - t0
+    return {"value": world * e * n * k / t, "ms_per_episode": t / k * 1e3,
+            "instances_per_gpu": b, "starts": n, "envs_per_gpu": e,
+            "bytes_per_env_step_decode_fused": 6 * n + 54,
+            "allgather_ms": t_ag * 1e3, "global_instances": m["instances"],
+            "loss": float(m["loss"]), "max_reward_mean": float(m["max_reward_mean"])}
 
 
 if __name__ == "__main__":

@@ -69,12 +69,14 @@ int co_tsp_step(int64_t batch, int64_t num_loc, const int64_t* action, const uin
                 int first_mode, const int32_t* first_flag, int32_t* status, void* stream);
 
 /* TSPEnv.get_reward (envs/common/base.py:182-188 + tsp/env.py:157-173):
- * reward[b] = -closed tour length of locs[b, actions[b, 0..T-1]].
+ * reward[b] = -closed tour length of locs[b % locs_batch, actions[b, 0..T-1]]
+ * (locs_batch = batch normally; = instances for the POMO [S, B] multistart layout,
+ * which then reads each instance's coordinates without batchify's copy, ops.py:16).
  * actions element (b, t) lives at actions[b*act_stride_b + t*act_stride_t].
  * check != 0: a row that is not a permutation of 0..T-1 sets CO_ST_INVALID_TOUR
  * (the reference's sort(1) == arange(T) test). */
 int co_tsp_reward(int64_t batch, int64_t num_loc, int64_t steps, const float* locs,
-                  const int64_t* actions, int64_t act_stride_b, int64_t act_stride_t, int check,
+                  int64_t locs_batch, const int64_t* actions, int64_t act_stride_b, int64_t act_stride_t, int check,
                   float* reward, int32_t* status, void* stream);
 
 /* ----------------------------------------------------------------- CVRP */
@@ -174,6 +176,21 @@ int co_decode_step(int64_t batch, int64_t n_actions, const float* logits, int64_
                    float* logprobs_full, uint64_t seed, uint64_t offset, int32_t* status,
                    void* stream);
 
+/* co_decode_step fused with TSPEnv._step (tsp/env.py:67-93) for the selected action:
+ * mask_out = mask_in minus the action (in-place NOT allowed), i_out = i_in + 1,
+ * first_out = first_mode ? action : first_in, done = nothing left, step_reward = 0,
+ * action_out / logp_sel as co_decode_step (action_out must not alias action_in);
+ * ll_accum (nullable) += logp_sel: get_log_likelihood's sum (decoding.py:39-65).
+ * The decode-fused env-step of SURVEY.md 8d (4N + 4 B on top of co_tsp_step). */
+int co_tsp_decode_step(int64_t batch, int64_t num_loc, const float* logits,
+                       int64_t logits_stride, const uint8_t* mask_in, float tanh_clipping,
+                       float temperature, int mode, const int64_t* action_in,
+                       int64_t* action_out, float* logp_sel, uint64_t seed, uint64_t offset,
+                       uint8_t* mask_out, const int64_t* i_in, int64_t* i_out,
+                       const int64_t* first_in, int64_t* first_out, int first_mode,
+                       uint8_t* done, uint8_t* step_reward, float* ll_accum, int32_t* status,
+                       void* stream);
+
 /* ------------------------------------------- bench policies (in-kernel) */
 
 /* Deterministic cheap policies for the env-throughput benchmark
@@ -219,6 +236,16 @@ int co_slap_rollout(int64_t batch, int64_t num_slots, int64_t n_products, int64_
                     int64_t* acts_out, uint8_t* action_mask, int32_t* assignment, int64_t* i,
                     uint8_t* done, uint8_t* step_reward, float* reward, float* ratio,
                     int32_t* status, void* stream);
+
+/* POMO shared baseline (rl4co/models/rl/reinforce/baselines.py:57-61,
+ * reinforce.py:97-115, zoo/pomo/model.py:105-114) over the multistart layout
+ * env e = s*instances + b: bl[b] = mean_s reward, max_reward[b] / best_start[b] =
+ * max / first argmax over s, adv[e] = reward[e] - bl[b] and
+ * loss_terms[b] = sum_s adv * log_likelihood (loss = -sum_b loss_terms / (S*B)).
+ * log_likelihood / adv / loss_terms may be NULL. */
+int co_pomo_shared_baseline(int64_t instances, int64_t starts, const float* reward,
+                            const float* log_likelihood, float* bl, float* max_reward,
+                            int64_t* best_start, float* adv, float* loss_terms, void* stream);
 
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);

@@ -25,7 +25,7 @@ _i64, _i32, _f32, _u64, _p = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctype
 _SIGS = {
     "co_tsp_reset": [_i64, _i64, _p, _p, _p, _p, _p, _p],
     "co_tsp_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p, _p],
-    "co_tsp_reward": [_i64, _i64, _i64, _p, _p, _i64, _i64, _i32, _p, _p, _p],
+    "co_tsp_reward": [_i64, _i64, _i64, _p, _i64, _p, _i64, _i64, _i32, _p, _p, _p],
     "co_cvrp_reset": [_i64, _i64, _p, _p, _p, _f32, _p, _p, _p, _p, _p, _p, _p],
     "co_cvrp_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "co_cvrp_action_mask": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p],
@@ -41,6 +41,9 @@ _SIGS = {
     "co_cvrp_nearest_action": [_i64, _i64, _p, _p, _p, _p, _p],
     "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],
     "co_count_not_done": [_p, _i64, _p, _p],
+    "co_pomo_shared_baseline": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
+    "co_tsp_decode_step": [_i64, _i64, _p, _i64, _p, _f32, _f32, _i32, _p, _p, _p, _u64, _u64, _p,
+                           _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p],
     "co_tsp_rollout": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
     "co_slap_rollout": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                         _p, _p, _p, _p],

@@ -55,7 +55,54 @@ __global__ __launch_bounds__(256) void count_not_done_kernel(const uint8_t* done
   if (lane_id() == 0 && c) atomicAdd(count, c);
 }
 
+// One wave per instance: lanes over the S starts (strided by `instances`).
+__global__ __launch_bounds__(256) void pomo_baseline_kernel(int64_t B, int S, const float* reward,
+                                                            const float* ll, float* bl,
+                                                            float* maxr, int64_t* best,
+                                                            float* adv, float* lterm) {
+  const int lane = lane_id();
+  const int64_t wpb = blockDim.x >> 6;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+       b += (int64_t)gridDim.x * wpb) {
+    float sum = 0.f, mv = -__builtin_inff();
+    int mi = 0x7fffffff;
+    for (int s = lane; s < S; s += 64) {
+      const float r = reward[(int64_t)s * B + b];
+      sum += r;
+      if (argmax_better(r, s, mv, mi)) { mv = r; mi = s; }
+    }
+    sum = wave_sum(sum);
+    wave_argmax(mv, mi);
+    const float mean = sum / (float)S;
+    float lt = 0.f;
+    for (int s = lane; s < S; s += 64) {
+      const int64_t e = (int64_t)s * B + b;
+      const float a = reward[e] - mean;
+      if (adv) adv[e] = a;
+      if (ll) lt += a * ll[e];
+    }
+    lt = wave_sum(lt);
+    if (lane == 0) {
+      bl[b] = mean;
+      if (maxr) maxr[b] = mv;
+      if (best) best[b] = mi;
+      if (lterm) lterm[b] = lt;
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int co_pomo_shared_baseline(int64_t B, int64_t S, const float* reward, const float* ll,
+                                       float* bl, float* maxr, int64_t* best, float* adv,
+                                       float* lterm, void* stream) {
+  if (B < 0 || S <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!reward || !bl || (lterm && !ll)) return CO_E_INVAL;
+  hipLaunchKernelGGL(pomo_baseline_kernel, dim3(grid_for(B, 4, 256 * 32)), dim3(256), 0,
+                     (hipStream_t)stream, B, (int)S, reward, ll, bl, maxr, best, adv, lterm);
+  return launch_status();
+}
 
 extern "C" const char* co_build_info(void) {
   return "rl4co_slap_amd co_env: gfx950 (CDNA4), wave64";

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
 
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void tsp_reward_kernel(int64_t B, int N, int T,
-                                                                const float2* locs,
+                                                                const float2* locs, int64_t LB,
                                                                 const int64_t* actions,
                                                                 int64_t sb, int64_t st, int check,
                                                                 float* reward, int32_t* status) {
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(WAVES * 64) void tsp_reward_kernel(int64_t B, int N
       __builtin_amdgcn_wave_barrier();
     }
     const int64_t* arow = actions + b * sb;
-    const float2* lrow = locs + b * (int64_t)N;
+    const float2* lrow = locs + (LB == B ? b : b % LB) * (int64_t)N;  // multistart: e % B
     double acc = 0.0;
     bool bad = false, range = false;
     for (int t = lane; t < T; t += 64) {
@@ -180,15 +180,16 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
 }
 
 extern "C" int co_tsp_reward(int64_t B, int64_t N, int64_t T, const float* locs,
-                             const int64_t* actions, int64_t sb, int64_t st, int check,
-                             float* reward, int32_t* status, void* stream) {
+                             int64_t locs_batch, const int64_t* actions, int64_t sb, int64_t st,
+                             int check, float* reward, int32_t* status, void* stream) {
   if (B < 0 || N <= 0 || T <= 0 || T > (1 << 24)) return CO_E_INVAL;
+  if (locs_batch <= 0 || (B > 0 && B % locs_batch != 0)) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!locs || !actions || !reward || (check && !status)) return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
   // step-major actions ([T, B], the stepwise engine's layout): thread per instance,
   // coalesced [B]-row loads, LDS-staged coordinates (rollout.hip)
-  if (sb == 1 && st == B && T == N && N <= 256 && B > 1 &&
+  if (sb == 1 && st == B && T == N && N <= 256 && B > 1 && locs_batch == B &&
       (reinterpret_cast<uintptr_t>(locs) & 15) == 0)
     return co_internal_tsp_reward_stepmajor(B, N, locs, actions, st, check, reward, status,
                                             stream);
@@ -198,8 +199,8 @@ extern "C" int co_tsp_reward(int64_t B, int64_t N, int64_t T, const float* locs,
   if (shmem > 64 * 1024) return CO_E_INVAL;
   hipLaunchKernelGGL(tsp_reward_kernel<W>, dim3(grid_for(B, W, 256 * 32)), dim3(W * 64), shmem,
                      (hipStream_t)stream, B, (int)N, (int)T,
-                     reinterpret_cast<const float2*>(locs), actions, sb, st, check, reward,
-                     status);
+                     reinterpret_cast<const float2*>(locs), locs_batch, actions, sb, st, check,
+                     reward, status);
   return launch_status();
 }
 

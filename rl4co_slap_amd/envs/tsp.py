@@ -100,7 +100,8 @@ class TSPEnv(RL4COEnvBase):
         b, t = actions.shape
         reward = torch.empty(b, dtype=torch.float32, device=locs.device)
         status = nat.scratch_status(locs.device)
-        nat.call("co_tsp_reward", b, locs.shape[-2], t, nat.ptr(locs), nat.ptr(actions),
+        nat.call("co_tsp_reward", b, locs.shape[-2], t, nat.ptr(locs), locs.shape[0],
+                 nat.ptr(actions),
                  actions.stride(0), actions.stride(1), int(check), nat.ptr(reward),
                  nat.ptr(status), nat.stream_of(locs))
         msgs = [(nat.ST_INVALID_TOUR, AssertionError, "Invalid tour")] if check else []

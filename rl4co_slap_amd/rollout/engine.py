@@ -90,7 +90,7 @@ class TSPStepwiseEpisode(_GraphEpisode):
                      nat.ptr(self.first[src]), nat.ptr(self.first[dst]), nat.ptr(self.cur),
                      nat.ptr(self.done), nat.ptr(self.step_reward), 1 if t == 0 else 0, None,
                      nat.ptr(self.status), s)
-        nat.call("co_tsp_reward", b, n, n, nat.ptr(self.locs), nat.ptr(self.acts), 1, b,
+        nat.call("co_tsp_reward", b, n, n, nat.ptr(self.locs), b, nat.ptr(self.acts), 1, b,
                  int(self.check), nat.ptr(self.reward), nat.ptr(self.status), s)
 
     def final_state(self):

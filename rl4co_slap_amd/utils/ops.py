@@ -113,7 +113,8 @@ def get_tour_length(ordered_locs: Tensor) -> Tensor:
     locs = ordered_locs.contiguous().float()
     ident = torch.arange(m, device=locs.device, dtype=torch.int64)
     out = torch.empty(b, dtype=torch.float32, device=locs.device)
-    nat.call("co_tsp_reward", b, m, m, nat.ptr(locs), nat.ptr(ident), 0, 1, 0, nat.ptr(out),
+    nat.call("co_tsp_reward", b, m, m, nat.ptr(locs), b, nat.ptr(ident), 0, 1, 0,
+             nat.ptr(out),
              None, nat.stream_of(locs))
     return -out
 
