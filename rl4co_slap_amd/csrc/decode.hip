@@ -2,9 +2,9 @@
 // tanh clip -> mask to -inf -> /temperature -> log_softmax -> greedy argmax |
 // Philox inverse-CDF sample | evaluate -> logp gather, in one pass.
 //
-// One wavefront per row (grid-stride); the row's N <= 64*NPL logits stay in
-// registers (NPL per lane), max / sum / argmax are wave reductions and the
-// sampling CDF is a wave inclusive scan.  log_softmax is evaluated with the
+// RL = 16/32/64 lanes per row (several rows per wave, grid-stride); the row's logits
+// stay in registers (EPL per lane), max / sum / argmax are xor-shuffle reductions
+// inside the lane group and the sampling CDF is a group inclusive scan.  log_softmax is evaluated with the
 // same association as ATen's CPU kernel: logp = (x - max) - log(sum(exp(x - max))),
 // so greedy ties resolve exactly like torch.argmax (first index).
 #include "co_common.hpp"
@@ -34,121 +34,218 @@ __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t offset, u
   return c0;
 }
 
-template <int NPL>
+// ---------------------------------------------------------------------------
+// Row engine: RL lanes per row (16, 32 or 64), 64/RL rows per wave, EPL elements per
+// lane (element c = sublane + RL*k).  All reductions are xor-shuffles inside the RL-lane
+// group; every lane of a wave runs the same number of row iterations (rows past B are
+// computed on dummy data and not stored), so the shuffles never see a partial group.
+template <int RL>
+__device__ __forceinline__ float grp_max(float v) {
+#pragma unroll
+  for (int off = RL / 2; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+template <int RL>
+__device__ __forceinline__ float grp_sum(float v) {
+#pragma unroll
+  for (int off = RL / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+template <int RL>
+__device__ __forceinline__ void grp_argmax(float& v, int& idx) {
+#pragma unroll
+  for (int off = RL / 2; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oi = __shfl_xor(idx, off, 64);
+    if (argmax_better(ov, oi, v, idx)) { v = ov; idx = oi; }
+  }
+}
+
+template <int RL>
+__device__ __forceinline__ int grp_min_int(int v) {
+#pragma unroll
+  for (int off = RL / 2; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
+  return v;
+}
+template <int RL>
+__device__ __forceinline__ int grp_max_int(int v) {
+#pragma unroll
+  for (int off = RL / 2; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Lane `sl` of the group owns the EPL consecutive elements c = sl*EPL + k.  VEC: the
+// row's logits are read as float4 and its mask bytes as u32 (needs N % 4 == 0 and a
+// 16-byte aligned logits row stride); otherwise scalar loads.
+template <int RL, int EPL, bool VEC>
+struct DecodeRow {
+  float x[EPL];     // log-probabilities after `run`
+  uint8_t mk[EPL];  // the row's action_mask bytes (1 when no mask)
+  int sel;          // selected action (valid on every lane of the group)
+  float lp;         // its log-probability
+  bool feas;        // mask[sel]
+
+  __device__ __forceinline__ void load(bool valid, int N, const float* lrow, const uint8_t* mrow,
+                                       int sl) {
+    const int c0 = sl * EPL;
+    if (VEC) {
+#pragma unroll
+      for (int j = 0; j < EPL / 4; ++j) {
+        const int c = c0 + 4 * j;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t mm = 0;
+        if (valid && c < N) {
+          v = *reinterpret_cast<const float4*>(lrow + c);
+          mm = mrow ? *reinterpret_cast<const uint32_t*>(mrow + c) : 0x01010101u;
+        }
+        x[4 * j] = v.x;
+        x[4 * j + 1] = v.y;
+        x[4 * j + 2] = v.z;
+        x[4 * j + 3] = v.w;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mk[4 * j + q] = (uint8_t)(mm >> (8 * q));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        const int c = c0 + k;
+        const bool in = valid && c < N;
+        x[k] = in ? lrow[c] : 0.f;
+        mk[k] = in ? (mrow ? mrow[c] : 1) : 0;
+      }
+    }
+  }
+
+  // tanh clip -> mask -> /T -> log_softmax -> select (decoding.py:141-191,371-399,489-499)
+  __device__ __forceinline__ void run(bool valid, int N, const float* lrow, const uint8_t* mrow,
+                                      float clip, float temp, int mode, int64_t a_in,
+                                      uint64_t seed, uint64_t offset, int64_t row, int sl,
+                                      int grp) {
+    const float NEG_INF = -__builtin_inff();
+    load(valid, N, lrow, mrow, sl);
+    const int c0 = sl * EPL;
+    float m = NEG_INF;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      float v = NEG_INF;
+      if (valid && c0 + k < N) {
+        v = x[k];
+        if (clip > 0.f) v = tanhf(v) * clip;
+        if (!mk[k]) v = NEG_INF;
+        v = v / temp;
+        m = fmaxf(m, v);
+      }
+      x[k] = v;
+    }
+    m = grp_max<RL>(m);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k)
+      if (valid && c0 + k < N) s += expf(x[k] - m);
+    s = grp_sum<RL>(s);
+    const float L = logf(s);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) x[k] = (x[k] - m) - L;  // ATen association
+    sel = 0;
+    if (mode == CO_DECODE_GREEDY) {
+      float bv = NEG_INF;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        const int c = c0 + k;
+        if (c < N && argmax_better(x[k], c, bv, bi)) { bv = x[k]; bi = c; }
+      }
+      grp_argmax<RL>(bv, bi);
+      sel = bi == 0x7fffffff ? 0 : bi;
+    } else if (mode == CO_DECODE_SAMPLING) {
+      // inverse CDF: lane partial sums, group exclusive scan, then the lane's own walk;
+      // the first element whose running sum passes u*total (and p > 0) is sampled
+      const uint32_t r = philox_u32(seed, offset, (uint64_t)row);
+      const float u = (float)(r >> 8) * (1.0f / 16777216.0f);
+      float p[EPL], own = 0.f;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        p[k] = (valid && c0 + k < N) ? expf(x[k]) : 0.f;
+        own += p[k];
+      }
+      float incl = own;
+#pragma unroll
+      for (int d = 1; d < RL; d <<= 1) {
+        const float t = __shfl_up(incl, d, RL);
+        if (sl >= d) incl += t;
+      }
+      const float total = __shfl(incl, grp * RL + RL - 1, 64);
+      const float target = u * total;
+      float run = incl - own;
+      int hit = 0x7fffffff, last = -1;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        run += p[k];
+        if (p[k] > 0.f) {
+          last = c0 + k;
+          if (run > target && hit == 0x7fffffff) hit = c0 + k;
+        }
+      }
+      hit = grp_min_int<RL>(hit);
+      last = grp_max_int<RL>(last);
+      sel = hit != 0x7fffffff ? hit : (last >= 0 ? last : 0);
+    } else {
+      sel = (a_in < 0 || a_in >= N) ? 0 : (int)a_in;
+    }
+    const int owner = grp * RL + sel / EPL, slot = sel % EPL;
+    float mine = 0.f;
+    int f = 0;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k)
+      if (k == slot) {
+        mine = x[k];
+        f = mk[k];
+      }
+    lp = __shfl(mine, owner, 64);
+    feas = __shfl(f, owner, 64) != 0;
+  }
+};
+
+template <int RL, int EPL, bool VEC>
 __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const float* logits,
                                                      int64_t lstride, const uint8_t* mask,
                                                      float clip, float temp, int mode,
                                                      const int64_t* action_in, int64_t* action_out,
                                                      float* logp_sel, float* full, uint64_t seed,
                                                      uint64_t offset, int32_t* status) {
-  const int lane = lane_id();
-  const int64_t wpb = blockDim.x >> 6;
-  const float NEG_INF = -__builtin_inff();
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
-       b += (int64_t)gridDim.x * wpb) {
-    const float* lrow = logits + b * lstride;
-    const uint8_t* mrow = mask ? mask + b * (int64_t)N : nullptr;
-    float x[NPL];
-    float m = NEG_INF;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const int c = lane + 64 * k;
-      float v = NEG_INF;
-      if (c < N) {
-        v = lrow[c];
-        if (clip > 0.f) v = tanhf(v) * clip;
-        if (mrow && !mrow[c]) v = NEG_INF;
-        v = v / temp;
-        m = fmaxf(m, v);
-      }
-      x[k] = v;
-    }
-    m = wave_max(m);
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k)
-      if (lane + 64 * k < N) s += expf(x[k] - m);
-    s = wave_sum(s);
-    const float L = logf(s);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) x[k] = (x[k] - m) - L;  // ATen association
+  constexpr int RPW = 64 / RL;
+  const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+    const int64_t row = base + grp;
+    const bool valid = row < B;
+    const int64_t r = valid ? row : 0;
+    const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
+    DecodeRow<RL, EPL, VEC> d;
+    d.run(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, clip, temp,
+          mode, a_in, seed, offset, row, sl, grp);
+    if (!valid) continue;
     if (full) {
 #pragma unroll
-      for (int k = 0; k < NPL; ++k)
-        if (lane + 64 * k < N) full[b * (int64_t)N + lane + 64 * k] = x[k];
+      for (int k = 0; k < EPL; ++k)
+        if (sl * EPL + k < N) full[r * (int64_t)N + sl * EPL + k] = d.x[k];
     }
-    int sel = 0;
-    if (mode == CO_DECODE_GREEDY) {
-      float bv = NEG_INF;
-      int bi = 0x7fffffff;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        const int c = lane + 64 * k;
-        if (c < N && argmax_better(x[k], c, bv, bi)) { bv = x[k]; bi = c; }
-      }
-      wave_argmax(bv, bi);
-      sel = bi;
-    } else if (mode == CO_DECODE_SAMPLING) {
-      const uint32_t r = philox_u32(seed, offset, (uint64_t)b);
-      const float u = (float)(r >> 8) * (1.0f / 16777216.0f);
-      float p[NPL];
-      float tot = 0.f;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        p[k] = (lane + 64 * k < N) ? expf(x[k]) : 0.f;
-        tot += p[k];
-      }
-      tot = wave_sum(tot);
-      const float target = u * tot;
-      float carry = 0.f;
-      int found = -1;
-      int lastpos = -1;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        float v = p[k];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const float t = __shfl_up(v, d, 64);
-          if (lane >= d) v += t;
-        }
-        const float cum = carry + v;
-        const bool hit = (p[k] > 0.f) && (cum > target);
-        const unsigned long long bal = __ballot(hit);
-        if (found < 0 && bal) found = 64 * k + __builtin_ctzll(bal);
-        const unsigned long long pos = __ballot(p[k] > 0.f);
-        if (pos) lastpos = 64 * k + 63 - __builtin_clzll(pos);
-        carry += __shfl(v, 63, 64);
-      }
-      sel = found >= 0 ? found : (lastpos >= 0 ? lastpos : 0);
-    } else {
-      const int64_t a = action_in[b];
-      sel = (a < 0 || a >= N) ? -1 : (int)a;
-      if (sel < 0 && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
-    }
-    // logp of the selected action: fetch from the owning lane's register
-    float lp = 0.f;
-    if (sel >= 0) {
-      const int owner = sel & 63, slot = sel >> 6;
-      float mine = 0.f;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k)
-        if (k == slot) mine = x[k];
-      lp = __shfl(mine, owner, 64);
-    }
-    if (lane == 0) {
-      if (mode != CO_DECODE_EVALUATE && mrow && !mrow[sel]) set_status(status, CO_ST_INFEASIBLE);
-      action_out[b] = mode == CO_DECODE_EVALUATE ? action_in[b] : (int64_t)sel;
-      if (logp_sel) logp_sel[b] = lp;
+    if (sl == 0) {
+      if (mode == CO_DECODE_EVALUATE && (a_in < 0 || a_in >= N))
+        set_status(status, CO_ST_INDEX_RANGE);
+      if (mode != CO_DECODE_EVALUATE && mask && !d.feas) set_status(status, CO_ST_INFEASIBLE);
+      action_out[r] = mode == CO_DECODE_EVALUATE ? a_in : (int64_t)d.sel;
+      if (logp_sel) logp_sel[r] = d.lp;
     }
   }
 }
 
-
 // Decode step fused with TSPEnv._step: the row's logits and action_mask are read once;
-// the selected action's env transition (tsp/env.py:67-93) is applied in the same wave:
-// mask_out = mask_in minus the action (the wave already holds the row), done = no bit
-// left (ballot), i + 1, first_node.  654 B per TSP-100 row-step.
-template <int NPL>
+// the selected action's env transition (tsp/env.py:67-93) is applied by the same lane
+// group: mask_out = mask_in minus the action, done = nothing left (group ballot),
+// i + 1, first_node.  654 B per TSP-100 row-step.
+template <int RL, int EPL, bool VEC>
 __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
     int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int mode,
@@ -158,123 +255,80 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
     const int64_t* __restrict__ first_in, int64_t* __restrict__ first_out, int take_first,
     uint8_t* __restrict__ done, uint8_t* __restrict__ step_reward, float* __restrict__ ll_accum,
     int32_t* status) {
-  const int lane = lane_id();
-  const int64_t wpb = blockDim.x >> 6;
-  const float NEG_INF = -__builtin_inff();
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
-       b += (int64_t)gridDim.x * wpb) {
-    const float* lrow = logits + b * lstride;
-    const uint8_t* mrow = mask_in + b * (int64_t)N;
-    float x[NPL];
-    uint8_t mk[NPL];
-    float m = NEG_INF;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const int c = lane + 64 * k;
-      float v = NEG_INF;
-      mk[k] = 0;
-      if (c < N) {
-        v = lrow[c];
-        mk[k] = mrow[c];
-        if (clip > 0.f) v = tanhf(v) * clip;
-        if (!mk[k]) v = NEG_INF;
-        v = v / temp;
-        m = fmaxf(m, v);
-      }
-      x[k] = v;
-    }
-    m = wave_max(m);
-    float sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k)
-      if (lane + 64 * k < N) sum += expf(x[k] - m);
-    sum = wave_sum(sum);
-    const float L = logf(sum);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) x[k] = (x[k] - m) - L;
-    int sel = 0;
-    if (mode == CO_DECODE_GREEDY) {
-      float bv = NEG_INF;
-      int bi = 0x7fffffff;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        const int c = lane + 64 * k;
-        if (c < N && argmax_better(x[k], c, bv, bi)) { bv = x[k]; bi = c; }
-      }
-      wave_argmax(bv, bi);
-      sel = bi;
-    } else if (mode == CO_DECODE_SAMPLING) {
-      const uint32_t r = philox_u32(seed, offset, (uint64_t)b);
-      const float u = (float)(r >> 8) * (1.0f / 16777216.0f);
-      float p[NPL], tot = 0.f;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        p[k] = (lane + 64 * k < N) ? expf(x[k]) : 0.f;
-        tot += p[k];
-      }
-      tot = wave_sum(tot);
-      const float target = u * tot;
-      float carry = 0.f;
-      int found = -1, lastpos = -1;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        float v = p[k];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const float t = __shfl_up(v, d, 64);
-          if (lane >= d) v += t;
-        }
-        const bool hit = (p[k] > 0.f) && (carry + v > target);
-        const unsigned long long bal = __ballot(hit);
-        if (found < 0 && bal) found = 64 * k + __builtin_ctzll(bal);
-        const unsigned long long pos = __ballot(p[k] > 0.f);
-        if (pos) lastpos = 64 * k + 63 - __builtin_clzll(pos);
-        carry += __shfl(v, 63, 64);
-      }
-      sel = found >= 0 ? found : (lastpos >= 0 ? lastpos : 0);
-    } else {
-      const int64_t a = action_in[b];
-      sel = (a < 0 || a >= N) ? 0 : (int)a;
-      if ((a < 0 || a >= N) && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
-    }
-    const int owner = sel & 63, slot = sel >> 6;
-    float mine = 0.f;
-    int feas = 0;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k)
-      if (k == slot) {
-        mine = x[k];
-        feas = mk[k];
-      }
-    const float lp = __shfl(mine, owner, 64);
-    feas = __shfl(feas, owner, 64);
-    // env step on the row the wave already holds
+  constexpr int RPW = 64 / RL;
+  const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
+  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+    const int64_t row = base + grp;
+    const bool valid = row < B;
+    const int64_t r = valid ? row : 0;
+    const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
+    // row scalars issued early, consumed after the decode math
+    const int64_t iv = valid ? i_in[r] : 0;
+    const int64_t fv = (valid && !take_first) ? first_in[r] : 0;
+    DecodeRow<RL, EPL, VEC> d;
+    d.run(valid, N, logits + r * lstride, mask_in + r * (int64_t)N, clip, temp, mode, a_in, seed,
+          offset, row, sl, grp);
     bool any_left = false;
-    uint8_t* orow = mask_out + b * (int64_t)N;
+    uint8_t* orow = mask_out + r * (int64_t)N;
+    const int c0 = sl * EPL;
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const int c = lane + 64 * k;
-      if (c < N) {
-        const uint8_t v = (c == sel) ? 0 : mk[k];
-        orow[c] = v;
-        any_left |= v != 0;
-      }
+    for (int k = 0; k < EPL; ++k) {
+      if (c0 + k == d.sel) d.mk[k] = 0;
+      any_left |= (valid && c0 + k < N && d.mk[k] != 0);
     }
-    const bool left = __any(any_left);
-    if (lane == 0) {
-      if (mode != CO_DECODE_EVALUATE && !feas) set_status(status, CO_ST_INFEASIBLE);
-      const int64_t a = mode == CO_DECODE_EVALUATE ? action_in[b] : (int64_t)sel;
-      action_out[b] = a;
-      if (logp_sel) logp_sel[b] = lp;
-      if (ll_accum) ll_accum[b] += lp;  // get_log_likelihood's sum, step by step
-      const int64_t iv = i_in[b];
-      i_out[b] = iv + 1;
-      first_out[b] = take_first ? a : first_in[b];
-      done[b] = !left;
-      step_reward[b] = 0;
+    if (VEC) {
+#pragma unroll
+      for (int j = 0; j < EPL / 4; ++j)
+        if (valid && c0 + 4 * j < N)
+          *reinterpret_cast<uint32_t*>(orow + c0 + 4 * j) =
+              (uint32_t)d.mk[4 * j] | ((uint32_t)d.mk[4 * j + 1] << 8) |
+              ((uint32_t)d.mk[4 * j + 2] << 16) | ((uint32_t)d.mk[4 * j + 3] << 24);
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k)
+        if (valid && c0 + k < N) orow[c0 + k] = d.mk[k];
+    }
+    const bool left = (__ballot(any_left) & gmask) != 0;
+    if (valid && sl == 0) {
+      if (mode == CO_DECODE_EVALUATE && (a_in < 0 || a_in >= N))
+        set_status(status, CO_ST_INDEX_RANGE);
+      if (mode != CO_DECODE_EVALUATE && !d.feas) set_status(status, CO_ST_INFEASIBLE);
+      const int64_t a = mode == CO_DECODE_EVALUATE ? a_in : (int64_t)d.sel;
+      action_out[r] = a;
+      if (logp_sel) logp_sel[r] = d.lp;
+      if (ll_accum) ll_accum[r] += d.lp;  // get_log_likelihood's sum, step by step
+      i_out[r] = iv + 1;
+      first_out[r] = take_first ? a : fv;
+      done[r] = !left;
+      step_reward[r] = 0;
     }
   }
 }
+
+// RL lanes x EPL consecutive elements per row: 16 x 4 up to N = 64, 32 x 4 up to 128,
+// 64 x 4 up to 256, then 64 x 8/16/32.
+#define CO_ROW_DISPATCH(LAUNCH, V)         \
+  if (N <= 64) LAUNCH(16, 4, V);           \
+  else if (N <= 128) LAUNCH(32, 4, V);     \
+  else if (N <= 256) LAUNCH(64, 4, V);     \
+  else if (N <= 512) LAUNCH(64, 8, V);     \
+  else if (N <= 1024) LAUNCH(64, 16, V);   \
+  else LAUNCH(64, 32, V)
+
+inline unsigned decode_grid(int64_t B, int N) {
+  const int rl = N <= 64 ? 16 : (N <= 128 ? 32 : 64);
+  const int64_t waves = (B * rl + 63) / 64;
+  return grid_for(waves, 4, 256 * 32);
+}
+
+inline bool decode_vec_ok(const float* logits, int64_t lstride, const uint8_t* mask, int64_t N) {
+  return (N % 4 == 0) && (lstride % 4 == 0) &&
+         ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(mask)) & 15) == 0;
+}
+
 }  // namespace
 
 extern "C" int co_decode_step(int64_t B, int64_t N, const float* logits, int64_t lstride,
@@ -287,18 +341,17 @@ extern "C" int co_decode_step(int64_t B, int64_t N, const float* logits, int64_t
   if (B == 0) return CO_OK;
   if (!logits || !action_out) return CO_E_INVAL;
   if (mode == CO_DECODE_EVALUATE && !action_in) return CO_E_INVAL;
-  const dim3 grid(grid_for(B, 4, 256 * 32)), block(256);
+  const dim3 grid(decode_grid(B, (int)N)), block(256);
   hipStream_t s = (hipStream_t)stream;
-#define CO_DECODE(NPL)                                                                         \
-  hipLaunchKernelGGL(decode_kernel<NPL>, grid, block, 0, s, B, (int)N, logits, lstride, mask, \
-                     clip, temp, mode, action_in, action_out, logp_sel, full, seed, offset,    \
-                     status)
-  if (N <= 64) CO_DECODE(1);
-  else if (N <= 128) CO_DECODE(2);
-  else if (N <= 256) CO_DECODE(4);
-  else if (N <= 512) CO_DECODE(8);
-  else if (N <= 1024) CO_DECODE(16);
-  else CO_DECODE(32);
+#define CO_DECODE(RL, EPL, V)                                                                  \
+  hipLaunchKernelGGL((decode_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N, logits,        \
+                     lstride, mask, clip, temp, mode, action_in, action_out, logp_sel, full,   \
+                     seed, offset, status)
+  if (decode_vec_ok(logits, lstride, mask, N)) {
+    CO_ROW_DISPATCH(CO_DECODE, true);
+  } else {
+    CO_ROW_DISPATCH(CO_DECODE, false);
+  }
 #undef CO_DECODE
   return launch_status();
 }
@@ -318,19 +371,19 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
       !done || !step_reward || (first_mode == 0 && !first_in) ||
       (mode == CO_DECODE_EVALUATE && !action_in))
     return CO_E_INVAL;
-  const dim3 grid(grid_for(B, 4, 256 * 32)), block(256);
+  const dim3 grid(decode_grid(B, (int)N)), block(256);
   hipStream_t s = (hipStream_t)stream;
-#define CO_TDS(NPL)                                                                            \
-  hipLaunchKernelGGL(tsp_decode_step_kernel<NPL>, grid, block, 0, s, B, (int)N, logits,        \
-                     lstride, mask_in, clip, temp, mode, action_in, action_out, logp_sel,      \
-                     seed, offset, mask_out, i_in, i_out, first_in, first_out, first_mode,     \
-                     done, step_reward, ll_accum, status)
-  if (N <= 64) CO_TDS(1);
-  else if (N <= 128) CO_TDS(2);
-  else if (N <= 256) CO_TDS(4);
-  else if (N <= 512) CO_TDS(8);
-  else if (N <= 1024) CO_TDS(16);
-  else CO_TDS(32);
+#define CO_TDS(RL, EPL, V)                                                                     \
+  hipLaunchKernelGGL((tsp_decode_step_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N,       \
+                     logits, lstride, mask_in, clip, temp, mode, action_in, action_out,        \
+                     logp_sel, seed, offset, mask_out, i_in, i_out, first_in, first_out,       \
+                     first_mode, done, step_reward, ll_accum, status)
+  if (decode_vec_ok(logits, lstride, mask_in, N) &&
+      (reinterpret_cast<uintptr_t>(mask_out) & 3) == 0) {
+    CO_ROW_DISPATCH(CO_TDS, true);
+  } else {
+    CO_ROW_DISPATCH(CO_TDS, false);
+  }
 #undef CO_TDS
   return launch_status();
 }

@@ -46,5 +46,10 @@ def test_pomo_episode_matches_oracle(dev, b, n):
         assert torch.allclose(st["bl_val"].cpu(), ref["bl_val"].squeeze(1), rtol=1e-5, atol=1e-5)
         assert torch.allclose(st["max_reward"].cpu(), ref["max_reward"], rtol=1e-5, atol=1e-6)
         loss = -st["loss_terms"].cpu().sum() / (b * s)
-        assert torch.allclose(loss, ref["loss"], rtol=1e-4, atol=1e-5)
+        # the loss is a cancelling sum: bound the error by the magnitude of its terms
+        from oracle.ops import unbatchify
+
+        rw, llr = unbatchify(out["reward"], s), unbatchify(out["log_likelihood"], s)
+        scale = ((rw - rw.mean(1, keepdim=True)).abs() * llr.abs()).mean()
+        assert (loss - ref["loss"]).abs() <= 1e-5 * scale + 1e-6
     assert st["done"].all() and not st["action_mask"].any()

@@ -1,0 +1,48 @@
+"""Diagnostic timing of the decode kernels (not part of the product)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rl4co_slap_amd import _native as nat  # noqa: E402
+
+nat.load()
+dev = torch.device("cuda:0")
+for B, N in [(102400, 100), (65536, 100), (102400, 20)]:
+    logits = torch.randn(B, N, device=dev)
+    mask = torch.rand(B, N, device=dev) > 0.3
+    mask[:, 0] = True
+    out_a = torch.empty(B, dtype=torch.int64, device=dev)
+    lp = torch.empty(B, device=dev)
+    m2 = torch.empty_like(mask)
+    i0 = torch.zeros(B, 1, dtype=torch.int64, device=dev)
+    i1 = torch.empty_like(i0)
+    f0 = torch.zeros(B, dtype=torch.int64, device=dev)
+    f1 = torch.empty_like(f0)
+    done = torch.empty(B, dtype=torch.bool, device=dev)
+    sr = torch.empty_like(done)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    for clip in (0.0, 10.0):
+        for name in ("decode", "tsp_decode"):
+            def run():
+                if name == "decode":
+                    nat.call("co_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, 0,
+                             None, nat.ptr(out_a), nat.ptr(lp), None, 0, 0, nat.ptr(st), s)
+                else:
+                    nat.call("co_tsp_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, 0,
+                             None, nat.ptr(out_a), nat.ptr(lp), 0, 0, nat.ptr(m2), nat.ptr(i0),
+                             nat.ptr(i1), nat.ptr(f0), nat.ptr(f1), 0, nat.ptr(done), nat.ptr(sr),
+                             None, nat.ptr(st), s)
+            for _ in range(5):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(50):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / 50
+            byts = B * (5 * N + 16) if name == "decode" else B * (6 * N + 54)
+            print(f"B={B} N={N} clip={clip} {name}: {us:.1f} us  {byts / us / 1e3:.0f} GB/s")
