@@ -11,6 +11,27 @@
 
 using namespace co;
 
+// decode tuning (tools/build_variants.sh sweeps them): lanes per row for each row-length
+// bucket N <= 16, 32, 64, 128, 256 (EPL = bucket / lanes); longer rows use 64 lanes
+#ifndef CO_RL16
+#define CO_RL16 4
+#endif
+#ifndef CO_RL32
+#define CO_RL32 4
+#endif
+#ifndef CO_RL64
+#define CO_RL64 8
+#endif
+#ifndef CO_RL128
+#define CO_RL128 16
+#endif
+#ifndef CO_RL256
+#define CO_RL256 32
+#endif
+#ifndef CO_DECODE_UNR
+#define CO_DECODE_UNR 1
+#endif
+
 namespace {
 
 // Philox-4x32-10 (Salmon et al. 2011), counter = (offset_lo, offset_hi, row_lo, row_hi).
@@ -35,43 +56,95 @@ __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t offset, u
 }
 
 // ---------------------------------------------------------------------------
-// Row engine: RL lanes per row (16, 32 or 64), 64/RL rows per wave, EPL elements per
-// lane (element c = sublane + RL*k).  All reductions are xor-shuffles inside the RL-lane
-// group; every lane of a wave runs the same number of row iterations (rows past B are
-// computed on dummy data and not stored), so the shuffles never see a partial group.
-template <int RL>
-__device__ __forceinline__ float grp_max(float v) {
-#pragma unroll
-  for (int off = RL / 2; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  return v;
+// Row engine: RL lanes per row (4 ... 64), 64/RL rows per wave, EPL consecutive
+// elements per lane.  Group reductions are butterflies without LDS traffic: DPP
+// quad_perm (xor 1, xor 2), row_half_mirror and row_mirror inside each 16-lane row,
+// then gfx950's v_permlane16_swap / v_permlane32_swap across rows.  The mirrors are not
+// xor partners but pair every lane with one in the other half, which is all a
+// commutative reduction needs.  Every lane of a wave runs the same number of row
+// iterations (rows past B run on dummy data and are not stored), so no stage reads an
+// inactive lane.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
 }
-template <int RL>
-__device__ __forceinline__ float grp_sum(float v) {
-#pragma unroll
-  for (int off = RL / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-template <int RL>
-__device__ __forceinline__ void grp_argmax(float& v, int& idx) {
-#pragma unroll
-  for (int off = RL / 2; off > 0; off >>= 1) {
-    const float ov = __shfl_xor(v, off, 64);
-    const int oi = __shfl_xor(idx, off, 64);
-    if (argmax_better(ov, oi, v, idx)) { v = ov; idx = oi; }
+
+// Reduce (value, aux) pairs with `take(ov, oa, v, a)` = "the other pair wins".
+template <int RL, class Take>
+__device__ __forceinline__ void grp_reduce2(uint32_t& v, uint32_t& a, Take take) {
+  uint32_t ov, oa;
+#define CO_DPP_STAGE(C)                      \
+  ov = dpp_u<C>(v);                          \
+  oa = dpp_u<C>(a);                          \
+  if (take(ov, oa, v, a)) { v = ov; a = oa; }
+  if (RL >= 2) { CO_DPP_STAGE(0xB1); }   // quad_perm [1,0,3,2]
+  if (RL >= 4) { CO_DPP_STAGE(0x4E); }   // quad_perm [2,3,0,1]
+  if (RL >= 8) { CO_DPP_STAGE(0x141); }  // row_half_mirror
+  if (RL >= 16) { CO_DPP_STAGE(0x140); } // row_mirror
+#undef CO_DPP_STAGE
+  if (RL >= 32) {
+    const auto rv = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    const auto ra = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    v = rv[0]; a = ra[0];
+    if (take(rv[1], ra[1], v, a)) { v = rv[1]; a = ra[1]; }
+  }
+  if (RL >= 64) {
+    const auto rv = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    const auto ra = __builtin_amdgcn_permlane32_swap(a, a, false, false);
+    v = rv[0]; a = ra[0];
+    if (take(rv[1], ra[1], v, a)) { v = rv[1]; a = ra[1]; }
   }
 }
 
+template <int RL, class Op>
+__device__ __forceinline__ uint32_t grp_reduce(uint32_t v, Op op) {
+  if (RL >= 2) v = op(v, dpp_u<0xB1>(v));
+  if (RL >= 4) v = op(v, dpp_u<0x4E>(v));
+  if (RL >= 8) v = op(v, dpp_u<0x141>(v));
+  if (RL >= 16) v = op(v, dpp_u<0x140>(v));
+  if (RL >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = op(r[0], r[1]);
+  }
+  if (RL >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = op(r[0], r[1]);
+  }
+  return v;
+}
+
+template <int RL>
+__device__ __forceinline__ float grp_max(float v) {
+  return __uint_as_float(grp_reduce<RL>(__float_as_uint(v), [](uint32_t x, uint32_t y) {
+    return __float_as_uint(fmaxf(__uint_as_float(x), __uint_as_float(y)));
+  }));
+}
+template <int RL>
+__device__ __forceinline__ float grp_sum(float v) {
+  return __uint_as_float(grp_reduce<RL>(__float_as_uint(v), [](uint32_t x, uint32_t y) {
+    return __float_as_uint(__uint_as_float(x) + __uint_as_float(y));
+  }));
+}
+template <int RL>
+__device__ __forceinline__ void grp_argmax(float& v, int& idx) {
+  uint32_t uv = __float_as_uint(v), ui = (uint32_t)idx;
+  grp_reduce2<RL>(uv, ui, [](uint32_t ov, uint32_t oi, uint32_t cv, uint32_t ci) {
+    return argmax_better(__uint_as_float(ov), (int)oi, __uint_as_float(cv), (int)ci);
+  });
+  v = __uint_as_float(uv);
+  idx = (int)ui;
+}
 template <int RL>
 __device__ __forceinline__ int grp_min_int(int v) {
-#pragma unroll
-  for (int off = RL / 2; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off, 64));
-  return v;
+  return (int)grp_reduce<RL>((uint32_t)v, [](uint32_t x, uint32_t y) {
+    return (uint32_t)min((int)x, (int)y);
+  });
 }
 template <int RL>
 __device__ __forceinline__ int grp_max_int(int v) {
-#pragma unroll
-  for (int off = RL / 2; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-  return v;
+  return (int)grp_reduce<RL>((uint32_t)v, [](uint32_t x, uint32_t y) {
+    return (uint32_t)max((int)x, (int)y);
+  });
 }
 
 // Lane `sl` of the group owns the EPL consecutive elements c = sl*EPL + k.  VEC: the
@@ -121,8 +194,15 @@ struct DecodeRow {
                                       float clip, float temp, int mode, int64_t a_in,
                                       uint64_t seed, uint64_t offset, int64_t row, int sl,
                                       int grp) {
-    const float NEG_INF = -__builtin_inff();
     load(valid, N, lrow, mrow, sl);
+    compute(valid, N, clip, temp, mode, a_in, seed, offset, row, sl, grp);
+  }
+
+  // the math on data already `load`ed (callers overlap several rows' loads)
+  __device__ __forceinline__ void compute(bool valid, int N, float clip, float temp, int mode,
+                                          int64_t a_in, uint64_t seed, uint64_t offset,
+                                          int64_t row, int sl, int grp) {
+    const float NEG_INF = -__builtin_inff();
     const int c0 = sl * EPL;
     float m = NEG_INF;
 #pragma unroll
@@ -245,7 +325,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
 // the selected action's env transition (tsp/env.py:67-93) is applied by the same lane
 // group: mask_out = mask_in minus the action, done = nothing left (group ballot),
 // i + 1, first_node.  654 B per TSP-100 row-step.
-template <int RL, int EPL, bool VEC>
+template <int RL, int EPL, bool VEC, int UNR = CO_DECODE_UNR>
 __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
     int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int mode,
@@ -260,67 +340,83 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
-    const int64_t row = base + grp;
-    const bool valid = row < B;
-    const int64_t r = valid ? row : 0;
-    const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
-    // row scalars issued early, consumed after the decode math
-    const int64_t iv = valid ? i_in[r] : 0;
-    const int64_t fv = (valid && !take_first) ? first_in[r] : 0;
-    DecodeRow<RL, EPL, VEC> d;
-    d.run(valid, N, logits + r * lstride, mask_in + r * (int64_t)N, clip, temp, mode, a_in, seed,
-          offset, row, sl, grp);
-    bool any_left = false;
-    uint8_t* orow = mask_out + r * (int64_t)N;
-    const int c0 = sl * EPL;
+  // UNR rows per lane group per iteration: every load of all UNR rows (logits, mask,
+  // i, first_node, action, ll accumulator) is issued before any row's math
+  for (int64_t base = wid * RPW * UNR; base < B; base += nwaves * RPW * UNR) {
+    DecodeRow<RL, EPL, VEC> d[UNR];
+    int64_t rr[UNR], ain[UNR], iv[UNR], fv[UNR];
+    bool vv[UNR];
+    float acc[UNR];
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      if (c0 + k == d.sel) d.mk[k] = 0;
-      any_left |= (valid && c0 + k < N && d.mk[k] != 0);
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t row = base + u * RPW + grp;
+      vv[u] = row < B;
+      rr[u] = vv[u] ? row : 0;
+      ain[u] = (mode == CO_DECODE_EVALUATE && vv[u]) ? action_in[rr[u]] : 0;
+      iv[u] = vv[u] ? i_in[rr[u]] : 0;
+      fv[u] = (vv[u] && !take_first) ? first_in[rr[u]] : 0;
+      acc[u] = (vv[u] && ll_accum) ? ll_accum[rr[u]] : 0.f;
+      d[u].load(vv[u], N, logits + rr[u] * lstride, mask_in + rr[u] * (int64_t)N, sl);
     }
-    if (VEC) {
 #pragma unroll
-      for (int j = 0; j < EPL / 4; ++j)
-        if (valid && c0 + 4 * j < N)
-          *reinterpret_cast<uint32_t*>(orow + c0 + 4 * j) =
-              (uint32_t)d.mk[4 * j] | ((uint32_t)d.mk[4 * j + 1] << 8) |
-              ((uint32_t)d.mk[4 * j + 2] << 16) | ((uint32_t)d.mk[4 * j + 3] << 24);
-    } else {
+    for (int u = 0; u < UNR; ++u) {
+      const bool valid = vv[u];
+      const int64_t r = rr[u], a_in = ain[u];
+      d[u].compute(valid, N, clip, temp, mode, a_in, seed, offset, base + u * RPW + grp, sl,
+                   grp);
+      bool any_left = false;
+      uint8_t* orow = mask_out + r * (int64_t)N;
+      const int c0 = sl * EPL;
 #pragma unroll
-      for (int k = 0; k < EPL; ++k)
-        if (valid && c0 + k < N) orow[c0 + k] = d.mk[k];
-    }
-    const bool left = (__ballot(any_left) & gmask) != 0;
-    if (valid && sl == 0) {
-      if (mode == CO_DECODE_EVALUATE && (a_in < 0 || a_in >= N))
-        set_status(status, CO_ST_INDEX_RANGE);
-      if (mode != CO_DECODE_EVALUATE && !d.feas) set_status(status, CO_ST_INFEASIBLE);
-      const int64_t a = mode == CO_DECODE_EVALUATE ? a_in : (int64_t)d.sel;
-      action_out[r] = a;
-      if (logp_sel) logp_sel[r] = d.lp;
-      if (ll_accum) ll_accum[r] += d.lp;  // get_log_likelihood's sum, step by step
-      i_out[r] = iv + 1;
-      first_out[r] = take_first ? a : fv;
-      done[r] = !left;
-      step_reward[r] = 0;
+      for (int k = 0; k < EPL; ++k) {
+        if (c0 + k == d[u].sel) d[u].mk[k] = 0;
+        any_left |= (valid && c0 + k < N && d[u].mk[k] != 0);
+      }
+      if (VEC) {
+#pragma unroll
+        for (int j = 0; j < EPL / 4; ++j)
+          if (valid && c0 + 4 * j < N)
+            *reinterpret_cast<uint32_t*>(orow + c0 + 4 * j) =
+                (uint32_t)d[u].mk[4 * j] | ((uint32_t)d[u].mk[4 * j + 1] << 8) |
+                ((uint32_t)d[u].mk[4 * j + 2] << 16) | ((uint32_t)d[u].mk[4 * j + 3] << 24);
+      } else {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k)
+          if (valid && c0 + k < N) orow[c0 + k] = d[u].mk[k];
+      }
+      const bool left = (__ballot(any_left) & gmask) != 0;
+      if (valid && sl == 0) {
+        if (mode == CO_DECODE_EVALUATE && (a_in < 0 || a_in >= N))
+          set_status(status, CO_ST_INDEX_RANGE);
+        if (mode != CO_DECODE_EVALUATE && !d[u].feas) set_status(status, CO_ST_INFEASIBLE);
+        const int64_t a = mode == CO_DECODE_EVALUATE ? a_in : (int64_t)d[u].sel;
+        action_out[r] = a;
+        if (logp_sel) logp_sel[r] = d[u].lp;
+        if (ll_accum) ll_accum[r] = acc[u] + d[u].lp;  // get_log_likelihood's sum, per step
+        i_out[r] = iv[u] + 1;
+        first_out[r] = take_first ? a : fv[u];
+        done[r] = !left;
+        step_reward[r] = 0;
+      }
     }
   }
 }
 
-// RL lanes x EPL consecutive elements per row: 16 x 4 up to N = 64, 32 x 4 up to 128,
-// 64 x 4 up to 256, then 64 x 8/16/32.
-#define CO_ROW_DISPATCH(LAUNCH, V)         \
-  if (N <= 64) LAUNCH(16, 4, V);           \
-  else if (N <= 128) LAUNCH(32, 4, V);     \
-  else if (N <= 256) LAUNCH(64, 4, V);     \
-  else if (N <= 512) LAUNCH(64, 8, V);     \
-  else if (N <= 1024) LAUNCH(64, 16, V);   \
+// RL lanes x EPL consecutive elements per row, by row-length bucket (CO_RL* above).
+#define CO_ROW_DISPATCH(LAUNCH, V)                           \
+  if (N <= 16) LAUNCH(CO_RL16, 16 / CO_RL16, V);             \
+  else if (N <= 32) LAUNCH(CO_RL32, 32 / CO_RL32, V);        \
+  else if (N <= 64) LAUNCH(CO_RL64, 64 / CO_RL64, V);        \
+  else if (N <= 128) LAUNCH(CO_RL128, 128 / CO_RL128, V);    \
+  else if (N <= 256) LAUNCH(CO_RL256, 256 / CO_RL256, V);    \
+  else if (N <= 512) LAUNCH(64, 8, V);                       \
+  else if (N <= 1024) LAUNCH(64, 16, V);                     \
   else LAUNCH(64, 32, V)
 
-inline unsigned decode_grid(int64_t B, int N) {
-  const int rl = N <= 64 ? 16 : (N <= 128 ? 32 : 64);
-  const int64_t waves = (B * rl + 63) / 64;
+inline unsigned decode_grid(int64_t B, int N, int unr = 1) {
+  const int rl = N <= 16 ? CO_RL16 : N <= 32 ? CO_RL32 : N <= 64 ? CO_RL64
+               : N <= 128 ? CO_RL128 : N <= 256 ? CO_RL256 : 64;
+  const int64_t waves = ((B + unr - 1) / unr * rl + 63) / 64;
   return grid_for(waves, 4, 256 * 32);
 }
 
@@ -371,7 +467,7 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
       !done || !step_reward || (first_mode == 0 && !first_in) ||
       (mode == CO_DECODE_EVALUATE && !action_in))
     return CO_E_INVAL;
-  const dim3 grid(decode_grid(B, (int)N)), block(256);
+  const dim3 grid(decode_grid(B, (int)N, CO_DECODE_UNR)), block(256);
   hipStream_t s = (hipStream_t)stream;
 #define CO_TDS(RL, EPL, V)                                                                     \
   hipLaunchKernelGGL((tsp_decode_step_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N,       \
