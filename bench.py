@@ -237,6 +237,8 @@ def main():
         # POMO TSP-100 (config 5): 1,024 instances x 100 starts per GPU, decode-fused steps
         # on HBM-resident logits, shared baseline + RCCL all-gather of per-instance results
         modes["pomo_tsp100"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev)
+        # CVRP-100 (config 3), nearest-feasible policy: fused episode and stepwise loop
+        modes.update(bench_cvrp(32768, 100, k, world, rank, dev))
         out["modes"] = modes
 
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -274,6 +276,38 @@ def bench_slap(b, k, world, rank, dev):
     t = max_over_ranks(wall, world, dev)
     out["slap_stepwise_graph"] = {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "bytes_per_env_step": 234}
+    return out
+
+
+def bench_cvrp(b, n, k, world, rank, dev):
+    """torch.manual_seed(1234 + rank); locs_all = rand(B, N+1, 2),
+    depot = locs_all[:, 0]; demand = ((rand(B, N) * 9).int() + 1) / 50 (CAPACITIES[100]).
+    env-steps = B x T, T = the batch-wide episode length the reference loop runs."""
+    from rl4co_slap_amd.rollout.engine import CVRPFusedEpisode, CVRPStepwiseEpisode
+
+    torch.manual_seed(1234 + rank)
+    locs_all = torch.rand(b, n + 1, 2)
+    demand = ((torch.rand(b, n) * 9).int() + 1).float() / 50.0
+    td = {"depot": locs_all[:, 0].contiguous().to(dev), "locs": locs_all[:, 1:].contiguous().to(dev),
+          "demand": demand.to(dev)}
+    out = {}
+    fu = CVRPFusedEpisode(td)
+    run = lambda: fu._launch(torch.cuda.current_stream(dev).cuda_stream)  # noqa: E731
+    wall, ev = timed(run, 4 * k, 2, world, dev)
+    st = fu.final_state()
+    T = st["steps"]
+    t = max_over_ranks(wall, world, dev)
+    out["cvrp_fused_nearest"] = {"value": world * b * T * 4 * k / t,
+                                 "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
+                                 "num_loc": n, "episode_steps": T,
+                                 "launch_us": ev / (4 * k) * 1e6}
+    sw = CVRPStepwiseEpisode(td).capture()
+    wall, ev = timed(sw.replay, k, 1, world, dev)
+    t = max_over_ranks(wall, world, dev)
+    assert sw.T == T
+    out["cvrp_stepwise_graph"] = {"value": world * b * T * k / t, "ms_per_episode": t / k * 1e3,
+                                  "batch_per_gpu": b, "episode_steps": T,
+                                  "bytes_per_env_step": 7 * n + 33}
     return out
 
 

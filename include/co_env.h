@@ -42,6 +42,7 @@ extern "C" {
 #define CO_ST_OVER_CAPACITY 2     /* "Used more than capacity"   cvrp/env.py:188-190 */
 #define CO_ST_INFEASIBLE 4        /* "infeasible action selected" decoding.py:376-379 */
 #define CO_ST_INDEX_RANGE 8       /* index out of range (torch raises IndexError/RuntimeError) */
+#define CO_ST_TRUNCATED 16        /* an episode hit max_steps before done (rollout max_steps) */
 
 /* Library identification: returns the gfx target string compiled in. */
 const char* co_build_info(void);
@@ -223,6 +224,25 @@ int co_tsp_rollout(int64_t batch, int64_t num_loc, const float* locs, const int6
                    int64_t* acts_out, uint8_t* action_mask, int64_t* first_node,
                    int64_t* current_node, int64_t* i, uint8_t* done, uint8_t* step_reward,
                    float* reward, int check, int32_t* status, void* stream);
+
+/* CVRP episode in one launch (cvrp/env.py:73-190 under decoding.py:88-109 rollout):
+ * reset from the generator columns (depot[B,2], locs[B,N,2], demand[B,N] already
+ * divided by the capacity, vehicle capacity vcap), then the nearest-feasible policy
+ * (co_cvrp_nearest_action's rule) until every instance is done, then the closed-tour
+ * reward.  Actions are step-major [max_steps, B]; *steps_out (device int32) receives
+ * the batch-wide episode length T (the reference's number of loop iterations); rows
+ * [len_b, T) of a shorter episode hold the depot steps the reference applies to
+ * finished instances, and their state reflects them.  Writes locs_out[B,N+1,2]
+ * (nullable), current_node[B], used_capacity[B], vehicle_capacity[B], visited[B,N+1],
+ * action_mask[B,N+1], done[B], step_reward[B] (bool 0), reward[B], len_out[B] (own
+ * episode length).  An instance not done after max_steps sets CO_ST_TRUNCATED.
+ * N <= 1023. */
+int co_cvrp_rollout(int64_t batch, int64_t num_loc, const float* depot, const float* locs,
+                    const float* demand, float vehicle_capacity, int64_t max_steps,
+                    int64_t* acts_out, float* locs_out, int64_t* current_node,
+                    float* used_capacity, float* vehicle_capacity_out, uint8_t* visited,
+                    uint8_t* action_mask, uint8_t* done, uint8_t* step_reward, float* reward,
+                    int32_t* len_out, int32_t* steps_out, int32_t* status, void* stream);
 
 /* SLAP episode in one launch (slap/env.py:38-143): P steps (product t <- the
  * step-t location; locations masked; done at i == P-1) then the per-order pick

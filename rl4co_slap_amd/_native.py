@@ -47,12 +47,15 @@ _SIGS = {
     "co_tsp_rollout": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
     "co_slap_rollout": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                         _p, _p, _p, _p],
+    "co_cvrp_rollout": [_i64, _i64, _p, _p, _p, _f32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                        _p, _p, _p, _p, _p],
 }
 
 ST_INVALID_TOUR = 1
 ST_OVER_CAPACITY = 2
 ST_INFEASIBLE = 4
 ST_INDEX_RANGE = 8
+ST_TRUNCATED = 16
 
 _lock = threading.Lock()
 _lib = None

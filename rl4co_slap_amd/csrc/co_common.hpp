@@ -69,6 +69,118 @@ __device__ __forceinline__ float edge_len(float x0, float y0, float x1, float y1
   return sqrtf(dx * dx + dy * dy);
 }
 
+// ---------------------------------------------------------------------------
+// Lane-group reductions for RL-lane groups (RL = 2 ... 64, 64/RL groups per wave),
+// without LDS traffic: DPP quad_perm (xor 1, xor 2), row_half_mirror and row_mirror
+// inside each 16-lane row, then gfx950's v_permlane16_swap / v_permlane32_swap across
+// rows.  The mirrors are not xor partners but pair every lane with one in the other
+// half, which is all a commutative reduction needs.  Every lane of the wave must be
+// active (callers keep wave-uniform loop counts).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+
+// Reduce (value, aux) pairs with `take(ov, oa, v, a)` = "the other pair wins".
+template <int RL, class Take>
+__device__ __forceinline__ void grp_reduce2(uint32_t& v, uint32_t& a, Take take) {
+  uint32_t ov, oa;
+#define CO_DPP_STAGE(C)                      \
+  ov = dpp_u<C>(v);                          \
+  oa = dpp_u<C>(a);                          \
+  if (take(ov, oa, v, a)) { v = ov; a = oa; }
+  if (RL >= 2) { CO_DPP_STAGE(0xB1); }   // quad_perm [1,0,3,2]
+  if (RL >= 4) { CO_DPP_STAGE(0x4E); }   // quad_perm [2,3,0,1]
+  if (RL >= 8) { CO_DPP_STAGE(0x141); }  // row_half_mirror
+  if (RL >= 16) { CO_DPP_STAGE(0x140); } // row_mirror
+#undef CO_DPP_STAGE
+  if (RL >= 32) {
+    const auto rv = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    const auto ra = __builtin_amdgcn_permlane16_swap(a, a, false, false);
+    v = rv[0]; a = ra[0];
+    if (take(rv[1], ra[1], v, a)) { v = rv[1]; a = ra[1]; }
+  }
+  if (RL >= 64) {
+    const auto rv = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    const auto ra = __builtin_amdgcn_permlane32_swap(a, a, false, false);
+    v = rv[0]; a = ra[0];
+    if (take(rv[1], ra[1], v, a)) { v = rv[1]; a = ra[1]; }
+  }
+}
+
+template <int RL, class Op>
+__device__ __forceinline__ uint32_t grp_reduce(uint32_t v, Op op) {
+  if (RL >= 2) v = op(v, dpp_u<0xB1>(v));
+  if (RL >= 4) v = op(v, dpp_u<0x4E>(v));
+  if (RL >= 8) v = op(v, dpp_u<0x141>(v));
+  if (RL >= 16) v = op(v, dpp_u<0x140>(v));
+  if (RL >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = op(r[0], r[1]);
+  }
+  if (RL >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = op(r[0], r[1]);
+  }
+  return v;
+}
+
+template <int RL>
+__device__ __forceinline__ float grp_max(float v) {
+  return __uint_as_float(grp_reduce<RL>(__float_as_uint(v), [](uint32_t x, uint32_t y) {
+    return __float_as_uint(fmaxf(__uint_as_float(x), __uint_as_float(y)));
+  }));
+}
+template <int RL>
+__device__ __forceinline__ float grp_sum(float v) {
+  return __uint_as_float(grp_reduce<RL>(__float_as_uint(v), [](uint32_t x, uint32_t y) {
+    return __float_as_uint(__uint_as_float(x) + __uint_as_float(y));
+  }));
+}
+template <int RL>
+__device__ __forceinline__ void grp_argmax(float& v, int& idx) {
+  uint32_t uv = __float_as_uint(v), ui = (uint32_t)idx;
+  grp_reduce2<RL>(uv, ui, [](uint32_t ov, uint32_t oi, uint32_t cv, uint32_t ci) {
+    return argmax_better(__uint_as_float(ov), (int)oi, __uint_as_float(cv), (int)ci);
+  });
+  v = __uint_as_float(uv);
+  idx = (int)ui;
+}
+template <int RL>
+__device__ __forceinline__ int grp_min_int(int v) {
+  return (int)grp_reduce<RL>((uint32_t)v, [](uint32_t x, uint32_t y) {
+    return (uint32_t)min((int)x, (int)y);
+  });
+}
+template <int RL>
+__device__ __forceinline__ int grp_max_int(int v) {
+  return (int)grp_reduce<RL>((uint32_t)v, [](uint32_t x, uint32_t y) {
+    return (uint32_t)max((int)x, (int)y);
+  });
+}
+
+template <int RL>
+__device__ __forceinline__ void grp_argmin(float& v, int& idx) {
+  uint32_t uv = __float_as_uint(v), ui = (uint32_t)idx;
+  grp_reduce2<RL>(uv, ui, [](uint32_t ov, uint32_t oi, uint32_t cv, uint32_t ci) {
+    const float a = __uint_as_float(ov), b = __uint_as_float(cv);
+    return a < b || (a == b && (int)oi < (int)ci);
+  });
+  v = __uint_as_float(uv);
+  idx = (int)ui;
+}
+
+// Zero a device int32 (flags / counters).  A kernel, not hipMemsetAsync: memset nodes
+// captured into HIP graphs were observed on MI355X to replay with a wrong fill byte
+// (0x10101010 after a 4-byte memset to 0), which corrupted counters in replays.
+namespace {  // one copy per translation unit
+__global__ void zero_i32_kernel(int32_t* p) { *p = 0; }
+}  // namespace
+inline int zero_i32(int32_t* p, hipStream_t s) {
+  hipLaunchKernelGGL(zero_i32_kernel, dim3(1), dim3(1), 0, s, p);
+  return (int)hipGetLastError();
+}
+
 // Grid size for grid-stride kernels: enough blocks to fill 256 CUs several times.
 inline unsigned grid_for(int64_t work_items, int per_block, int64_t cap = 256 * 16) {
   int64_t g = (work_items + per_block - 1) / per_block;
@@ -88,3 +200,8 @@ inline int launch_status() {
 int co_internal_tsp_reward_stepmajor(int64_t B, int64_t N, const float* locs,
                                      const int64_t* acts, int64_t st, int check, float* reward,
                                      int32_t* status, void* stream);
+// internal: nearest.hip's register-resident nearest-policy TSP episode
+int co_internal_tsp_nearest_rollout(int64_t B, int64_t N, const float* locs, int64_t* acts_out,
+                                    uint8_t* mask_out, int64_t* first_out, int64_t* cur_out,
+                                    int64_t* i_out, uint8_t* done_out, uint8_t* step_reward_out,
+                                    float* reward_out, void* stream);

@@ -1,0 +1,298 @@
+// Fused nearest-policy episodes for gfx950: the whole env-only rollout
+// (rl4co/utils/decoding.py:88-109) of TSP (tsp/env.py:67-173) and CVRP
+// (cvrp/env.py:73-190) with the nearest-node bench policy of SURVEY.md 8d in-kernel.
+//
+// Layout: a G-lane group per instance, 64/G instances per wavefront.  Lane `sl` of
+// the group keeps nodes c = sl + G*k (k < EPL) in VGPRs for the whole episode:
+// coordinates, CVRP demand, and a visited bit per node.  One policy step is EPL
+// distance evaluations per lane, a DPP / permlane-swap argmin over the group and
+// three lane broadcasts (x, y, demand of the chosen node); nothing is read from
+// memory after the first load and the only per-step store is the step-major action.
+// The oracle's policy (oracle/envs.py tsp_nearest_action / cvrp_nearest_action):
+// argmin over feasible nodes of f32 sqrt(dx*dx + dy*dy), ties -> lowest index.
+#include "co_common.hpp"
+
+using namespace co;
+
+namespace {
+
+constexpr int kNoNode = 0x7fffffff;
+
+template <int EPL>
+__device__ __forceinline__ float pick(const float (&v)[EPL], int slot) {
+  float r = 0.f;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) r = (k == slot) ? v[k] : r;
+  return r;
+}
+
+// TSP: step 0 takes node 0, steps 1..N-1 the nearest unvisited node.
+template <int G, int EPL>
+__global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
+    int64_t B, int N, const float2* __restrict__ locs, int64_t* __restrict__ acts_out,
+    uint8_t* __restrict__ mask_out, int64_t* __restrict__ first_out,
+    int64_t* __restrict__ cur_out, int64_t* __restrict__ i_out, uint8_t* __restrict__ done_out,
+    uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out) {
+  constexpr int IPW = 64 / G;
+  const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (int64_t base = wid * IPW; base < B; base += nwaves * IPW) {
+    const int64_t b = base + lane / G;
+    const bool valid = b < B;
+    const int64_t bb = valid ? b : 0;
+    const float2* lrow = locs + bb * N;
+    float px[EPL], py[EPL];
+    uint32_t vis = 0;  // bit k: node sl + G*k visited (or past N)
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const int c = sl + G * k;
+      const float2 q = c < N ? lrow[c] : make_float2(0.f, 0.f);
+      px[k] = q.x;
+      py[k] = q.y;
+      if (c >= N) vis |= 1u << k;
+    }
+    if (sl == 0) vis |= 1u;  // step 0: node 0
+    const float x0 = __shfl(px[0], gbase, 64), y0 = __shfl(py[0], gbase, 64);
+    float cx = x0, cy = y0;
+    if (valid && sl == 0) acts_out[bb] = 0;
+    double len = 0.0;
+    int cur = 0;
+    for (int t = 1; t < N; ++t) {
+      float best = __builtin_inff();
+      int bi = kNoNode;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        const float d = edge_len(cx, cy, px[k], py[k]);
+        if (!((vis >> k) & 1u) && d < best) {
+          best = d;
+          bi = sl + G * k;
+        }
+      }
+      grp_argmin<G>(best, bi);  // t < N: an unvisited node remains
+      const int owner = bi % G, slot = bi / G;
+      if (sl == owner) vis |= 1u << slot;
+      cx = __shfl(pick(px, slot), gbase + owner, 64);
+      cy = __shfl(pick(py, slot), gbase + owner, 64);
+      len += (double)best;
+      cur = bi;
+      if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = bi;
+    }
+    len += (double)edge_len(cx, cy, x0, y0);
+    if (!valid) continue;
+    uint8_t* mrow = mask_out + bb * N;
+    for (int c = sl; c < N; c += G) mrow[c] = 0;  // every node visited
+    if (sl == 0) {
+      first_out[bb] = 0;
+      cur_out[bb] = cur;
+      i_out[bb] = N;
+      done_out[bb] = 1;
+      step_reward_out[bb] = 0;
+      reward_out[bb] = -(float)len;
+    }
+  }
+}
+
+// CVRP: nodes 0..N (0 = depot).  Each step the nearest customer that is unvisited and
+// fits (!(demand + used > capacity), cvrp/env.py:140), else the depot; the env
+// transition of cvrp/env.py:73-105 on group-uniform scalars: used = (used + d) *
+// (a != 0), done = every node visited (visited.sum == N + 1, so the depot must have
+// been entered once).  A finished instance stops; co_cvrp_rollout's pad pass then
+// applies the reference's remaining depot steps up to the batch-wide episode length.
+template <int G, int EPL>
+__global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
+    int64_t B, int N, const float2* __restrict__ depot, const float2* __restrict__ locs_in,
+    const float* __restrict__ demand, float vcap, int max_steps, int64_t* __restrict__ acts_out,
+    float2* __restrict__ locs_out, int64_t* __restrict__ cur_out, float* __restrict__ used_out,
+    float* __restrict__ vcap_out, uint8_t* __restrict__ visited_out,
+    uint8_t* __restrict__ mask_out, uint8_t* __restrict__ done_out,
+    uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out,
+    int32_t* __restrict__ len_out, int32_t* __restrict__ tmax, int32_t* status) {
+  constexpr int IPW = 64 / G;
+  const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
+  const int M = N + 1;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (int64_t base = wid * IPW; base < B; base += nwaves * IPW) {
+    const int64_t b = base + lane / G;
+    const bool valid = b < B;
+    const int64_t bb = valid ? b : 0;
+    const float2* lrow = locs_in + bb * N;
+    const float* drow = demand + bb * N;
+    const float2 dep = depot[bb];
+    float px[EPL], py[EPL], dm[EPL];
+    uint32_t vis = 0;  // bit k: node sl + G*k visited (or past N)
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const int c = sl + G * k;
+      float2 q = make_float2(0.f, 0.f);
+      float d = 0.f;
+      if (c == 0) {
+        q = dep;
+      } else if (c <= N) {
+        q = lrow[c - 1];
+        d = drow[c - 1];
+      }
+      px[k] = q.x;
+      py[k] = q.y;
+      dm[k] = d;
+      if (c > N) vis |= 1u << k;
+      if (valid && locs_out && c <= N) locs_out[bb * M + c] = q;
+    }
+    float cx = dep.x, cy = dep.y, used = 0.f;
+    int cur = 0, ncust = 0, len = 0;
+    bool depot_seen = false, done = false;
+    double dist = 0.0;
+    for (int t = 0; t < max_steps; ++t) {
+      if (__ballot(!done) == 0) break;  // wave-uniform: the group reductions need every lane
+      float best = __builtin_inff();
+      int bi = kNoNode;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        const int c = sl + G * k;
+        const bool feas = c >= 1 && !((vis >> k) & 1u) && !(dm[k] + used > vcap);
+        const float d = edge_len(cx, cy, px[k], py[k]);
+        if (feas && d < best) {
+          best = d;
+          bi = c;
+        }
+      }
+      grp_argmin<G>(best, bi);
+      if (done) continue;
+      const int a = bi == kNoNode ? 0 : bi;
+      const int owner = a % G, slot = a / G;
+      const float ax = __shfl(pick(px, slot), gbase + owner, 64);
+      const float ay = __shfl(pick(py, slot), gbase + owner, 64);
+      const float ad = __shfl(pick(dm, slot), gbase + owner, 64);
+      if (sl == owner) vis |= 1u << slot;
+      dist += (double)(a == 0 ? edge_len(cx, cy, ax, ay) : best);
+      used = a != 0 ? (used + ad) * 1.0f : 0.0f;  // cvrp/env.py:83-85
+      ncust += a != 0;
+      depot_seen |= a == 0;
+      cur = a;
+      cx = ax;
+      cy = ay;
+      if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
+      len = t + 1;
+      done = ncust == N && depot_seen;
+    }
+    dist += (double)edge_len(cx, cy, dep.x, dep.y);  // closing edge to the depot
+    // final state rows: visited and get_action_mask (cvrp/env.py:137-149)
+    bool any_feas = false;
+    uint8_t* vrow = visited_out + bb * M;
+    uint8_t* mrow = mask_out + bb * M;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const int c = sl + G * k;
+      const bool v = (vis >> k) & 1u;
+      const bool feas = c >= 1 && c <= N && !v && !(dm[k] + used > vcap);
+      any_feas |= feas;
+      if (valid && c <= N) {
+        vrow[c] = v;
+        if (c >= 1) mrow[c] = feas;
+      }
+    }
+    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+    const bool anyf = (__ballot(any_feas) & gmask) != 0;
+    if (valid && sl == 0) {
+      mrow[0] = !((cur == 0) && anyf);
+      cur_out[bb] = cur;
+      used_out[bb] = used;
+      vcap_out[bb] = vcap;
+      done_out[bb] = done;
+      step_reward_out[bb] = 0;
+      reward_out[bb] = -(float)dist;
+      len_out[bb] = len;
+      if (!done) set_status(status, CO_ST_TRUNCATED);
+      atomicMax(tmax, len);
+    }
+  }
+}
+
+// The reference keeps stepping finished instances until every instance is done
+// (constructive/base.py:230): their action is the depot (no customer fits), which
+// sets current_node = 0 and used_capacity = 0 and leaves visited / the mask as they
+// are.  Pads actions [len_b, T) with 0 and applies that state.
+__global__ __launch_bounds__(256) void cvrp_pad_kernel(int64_t B, const int32_t* __restrict__ len,
+                                                       const int32_t* __restrict__ tmax,
+                                                       int64_t* __restrict__ acts_out,
+                                                       int64_t* __restrict__ cur_out,
+                                                       float* __restrict__ used_out) {
+  const int T = *tmax;
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < B;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    const int L = len[b];
+    for (int t = L; t < T; ++t) acts_out[(int64_t)t * B + b] = 0;
+    if (L < T) {
+      cur_out[b] = 0;
+      used_out[b] = 0.f;
+    }
+  }
+}
+
+inline unsigned group_grid(int64_t B, int G) {
+  const int64_t waves = (B * G + 63) / 64;
+  return grid_for(waves, 4, 256 * 32);
+}
+
+}  // namespace
+
+// Called by co_tsp_rollout for the nearest policy (acts_in == NULL).
+int co_internal_tsp_nearest_rollout(int64_t B, int64_t N, const float* locs, int64_t* acts_out,
+                                    uint8_t* mask_out, int64_t* first_out, int64_t* cur_out,
+                                    int64_t* i_out, uint8_t* done_out, uint8_t* step_reward_out,
+                                    float* reward_out, void* stream) {
+  const float2* l2 = reinterpret_cast<const float2*>(locs);
+  hipStream_t s = (hipStream_t)stream;
+#define CO_TSPN(G, EPL)                                                                        \
+  hipLaunchKernelGGL((tsp_nearest_episode_kernel<G, EPL>), dim3(group_grid(B, G)), dim3(256),  \
+                     0, s, B, (int)N, l2, acts_out, mask_out, first_out, cur_out, i_out,       \
+                     done_out, step_reward_out, reward_out)
+  if (N <= 32) CO_TSPN(4, 8);
+  else if (N <= 64) CO_TSPN(8, 8);
+  else if (N <= 128) CO_TSPN(16, 8);
+  else if (N <= 256) CO_TSPN(32, 8);
+  else if (N <= 512) CO_TSPN(64, 8);
+  else CO_TSPN(64, 16);
+#undef CO_TSPN
+  return launch_status();
+}
+
+extern "C" int co_cvrp_rollout(int64_t B, int64_t N, const float* depot, const float* locs,
+                               const float* demand, float vcap, int64_t max_steps,
+                               int64_t* acts_out, float* locs_out, int64_t* cur_out,
+                               float* used_out, float* vcap_out, uint8_t* visited_out,
+                               uint8_t* mask_out, uint8_t* done_out, uint8_t* step_reward_out,
+                               float* reward_out, int32_t* len_out, int32_t* steps_out,
+                               int32_t* status, void* stream) {
+  if (B < 0 || N <= 0 || N > 1023 || max_steps <= 0 || max_steps > (1 << 30)) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!depot || !locs || !demand || !acts_out || !cur_out || !used_out || !vcap_out ||
+      !visited_out || !mask_out || !done_out || !step_reward_out || !reward_out || !len_out ||
+      !steps_out || !status)
+    return CO_E_INVAL;
+  if ((reinterpret_cast<uintptr_t>(depot) | reinterpret_cast<uintptr_t>(locs) |
+       reinterpret_cast<uintptr_t>(locs_out)) & 7)
+    return CO_E_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  if (zero_i32(steps_out, s) != hipSuccess) return launch_status();
+  const float2* d2 = reinterpret_cast<const float2*>(depot);
+  const float2* l2 = reinterpret_cast<const float2*>(locs);
+  float2* lo = reinterpret_cast<float2*>(locs_out);
+#define CO_CVRPN(G, EPL)                                                                       \
+  hipLaunchKernelGGL((cvrp_nearest_episode_kernel<G, EPL>), dim3(group_grid(B, G)), dim3(256), \
+                     0, s, B, (int)N, d2, l2, demand, vcap, (int)max_steps, acts_out, lo,      \
+                     cur_out, used_out, vcap_out, visited_out, mask_out, done_out,             \
+                     step_reward_out, reward_out, len_out, steps_out, status)
+  const int64_t M = N + 1;
+  if (M <= 32) CO_CVRPN(4, 8);
+  else if (M <= 64) CO_CVRPN(8, 8);
+  else if (M <= 128) CO_CVRPN(16, 8);
+  else if (M <= 256) CO_CVRPN(32, 8);
+  else if (M <= 512) CO_CVRPN(64, 8);
+  else CO_CVRPN(64, 16);
+#undef CO_CVRPN
+  hipLaunchKernelGGL(cvrp_pad_kernel, dim3(grid_for(B, 256, 2048)), dim3(256), 0, s, B, len_out,
+                     steps_out, acts_out, cur_out, used_out);
+  return launch_status();
+}

@@ -140,8 +140,8 @@ extern "C" int co_gather_by_index(const void* src, int64_t outer, int64_t src_le
 extern "C" int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t* flag,
                              void* stream) {
   if (n < 0 || !flag) return CO_E_INVAL;
-  hipError_t e = hipMemsetAsync(flag, 0, sizeof(int32_t), (hipStream_t)stream);
-  if (e != hipSuccess) return (int)e;
+  const int e = zero_i32(flag, (hipStream_t)stream);
+  if (e != hipSuccess) return e;
   if (n == 0) return CO_OK;
   if (!x) return CO_E_INVAL;
   hipLaunchKernelGGL(any_eq_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0,
@@ -151,8 +151,8 @@ extern "C" int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t
 
 extern "C" int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream) {
   if (n < 0 || !count) return CO_E_INVAL;
-  hipError_t e = hipMemsetAsync(count, 0, sizeof(int32_t), (hipStream_t)stream);
-  if (e != hipSuccess) return (int)e;
+  const int e = zero_i32(count, (hipStream_t)stream);
+  if (e != hipSuccess) return e;
   if (n == 0) return CO_OK;
   if (!done) return CO_E_INVAL;
   hipLaunchKernelGGL(count_not_done_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0,

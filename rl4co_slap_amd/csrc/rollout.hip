@@ -527,6 +527,9 @@ extern "C" int co_tsp_rollout(int64_t B, int64_t N, const float* locs, const int
       !reward_out || (nearest && !acts_out) || (check && !status))
     return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  if (nearest)  // register-resident lane-group episode (nearest.hip)
+    return co_internal_tsp_nearest_rollout(B, N, locs, acts_out, mask_out, first_out, cur_out,
+                                           i_out, done_out, step_reward_out, reward_out, stream);
   if (reinterpret_cast<uintptr_t>(locs) & 15) return CO_E_ALIGN;  // LDS-DMA staging
   const int NW = (int)((N + 63) / 64);
   const size_t shmem = (size_t)kRollT * (nearest ? (N | 1) : N) * 8 +
@@ -543,15 +546,9 @@ extern "C" int co_tsp_rollout(int64_t B, int64_t N, const float* locs, const int
                        acts_in, acts_out, mask_out, first_out, cur_out, i_out, done_out,       \
                        step_reward_out, reward_out, check, status);                            \
   } while (0)
-  if (nearest) {
-    if (NW == 1) CO_ROLL(1, true);
-    else if (NW == 2) CO_ROLL(2, true);
-    else CO_ROLL(4, true);
-  } else {
-    if (NW == 1) CO_ROLL(1, false);
-    else if (NW == 2) CO_ROLL(2, false);
-    else CO_ROLL(4, false);
-  }
+  if (NW == 1) CO_ROLL(1, false);
+  else if (NW == 2) CO_ROLL(2, false);
+  else CO_ROLL(4, false);
 #undef CO_ROLL
   return launch_status();
 }

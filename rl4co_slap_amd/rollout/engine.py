@@ -238,3 +238,166 @@ class SLAPFusedEpisode(_GraphEpisode):
     def final_state(self):
         return {"action_mask": self.mask, "i": self.i, "assignment": self.assign,
                 "done": self.done, "reward": self.reward, "actions": self.acts.t()}
+
+
+class CVRPFusedEpisode(_GraphEpisode):
+    """The whole CVRP episode as ONE C-ABI call (``co_cvrp_rollout``): reset from the
+    generator columns, the nearest-feasible policy until every instance is done, the
+    reference's trailing depot steps for early finishers, and the closed-tour reward.
+
+    ``td`` holds the generator columns (``depot [B,2]``, ``locs [B,N,2]``, ``demand
+    [B,N]`` already divided by the capacity); ``vehicle_capacity`` is the env's
+    (``cvrp/env.py:126``, ``generator.vehicle_capacity``)."""
+
+    def __init__(self, td, vehicle_capacity: float = 1.0, max_steps: int = None,
+                 write_locs: bool = True):
+        locs = td["locs"]
+        super().__init__(locs.device)
+        d = locs.device
+        b, n = locs.shape[0], locs.shape[1]
+        self.b, self.n, self.vcap = b, n, float(vehicle_capacity)
+        self.max_steps = int(max_steps) if max_steps is not None else 2 * n + 1
+        self.depot = td["depot"].contiguous()
+        self.locs_in = locs.contiguous()
+        self.demand = td["demand"].contiguous()
+        self.acts = torch.empty((self.max_steps, b), dtype=torch.int64, device=d)
+        self.locs = torch.empty((b, n + 1, 2), dtype=torch.float32, device=d) if write_locs else None
+        self.cur = torch.empty((b, 1), dtype=torch.int64, device=d)
+        self.used = torch.empty((b, 1), dtype=torch.float32, device=d)
+        self.vcap_t = torch.empty((b, 1), dtype=torch.float32, device=d)
+        self.visited = torch.empty((b, n + 1), dtype=torch.uint8, device=d)
+        self.mask = torch.empty((b, n + 1), dtype=torch.bool, device=d)
+        self.done = torch.empty(b, dtype=torch.bool, device=d)
+        self.step_reward = torch.empty(b, dtype=torch.bool, device=d)
+        self.reward = torch.empty(b, dtype=torch.float32, device=d)
+        self.lens = torch.empty(b, dtype=torch.int32, device=d)
+        self.steps = torch.zeros(1, dtype=torch.int32, device=d)
+        self.status = torch.zeros(1, dtype=torch.int32, device=d)
+
+    def _launch(self, s):
+        nat.call("co_cvrp_rollout", self.b, self.n, nat.ptr(self.depot), nat.ptr(self.locs_in),
+                 nat.ptr(self.demand), self.vcap, self.max_steps, nat.ptr(self.acts),
+                 nat.ptr(self.locs), nat.ptr(self.cur), nat.ptr(self.used), nat.ptr(self.vcap_t),
+                 nat.ptr(self.visited), nat.ptr(self.mask), nat.ptr(self.done),
+                 nat.ptr(self.step_reward), nat.ptr(self.reward), nat.ptr(self.lens),
+                 nat.ptr(self.steps), nat.ptr(self.status), s)
+
+    def final_state(self):
+        """Post-rollout columns; reads the episode length (one host sync)."""
+        t = int(self.steps.item())
+        if int(self.status.item()) & nat.ST_TRUNCATED:
+            raise RuntimeError(f"CVRP rollout: an instance was not done after {self.max_steps} steps")
+        return {"locs": self.locs, "current_node": self.cur, "used_capacity": self.used,
+                "vehicle_capacity": self.vcap_t, "visited": self.visited,
+                "action_mask": self.mask, "done": self.done, "reward": self.reward,
+                "actions": self.acts[:t].t(), "steps": t}
+
+
+class CVRPStepwiseEpisode:
+    """Reference-shaped CVRP loop: one ``co_cvrp_nearest_action`` + ``co_cvrp_step``
+    launch pair per env step with the TensorDict state in HBM, ``while not
+    done.all()`` replaced by graph chunks and a device-side not-done count per step
+    (``co_count_not_done``) read once per chunk.  No instance can finish before N
+    steps, so steps 0..N-1 are one graph; later chunks are ``chunk`` steps.  Per-step
+    ``current_node``/``used_capacity`` rows are kept, so the state at the exact
+    all-done step T is returned even when the last chunk runs past it (steps after T
+    only repeat the depot action)."""
+
+    def __init__(self, td, vehicle_capacity: float = 1.0, max_steps: int = None,
+                 chunk: int = 8):
+        locs = td["locs"]
+        d = locs.device
+        self.device = d
+        b, n = locs.shape[0], locs.shape[1]
+        self.b, self.n, self.vcap, self.chunk = b, n, float(vehicle_capacity), chunk
+        self.max_steps = int(max_steps) if max_steps is not None else 2 * n + 1
+        T = self.max_steps
+        self.depot = td["depot"].contiguous()
+        self.locs_in = locs.contiguous()
+        self.demand = td["demand"].contiguous()
+        self.locs = torch.empty((b, n + 1, 2), dtype=torch.float32, device=d)
+        self.acts = torch.empty((T, b), dtype=torch.int64, device=d)
+        self.cur = torch.empty((T + 1, b), dtype=torch.int64, device=d)
+        self.used = torch.empty((T + 1, b), dtype=torch.float32, device=d)
+        self.vcap_t = torch.empty((b, 1), dtype=torch.float32, device=d)
+        self.visited = [torch.empty((b, n + 1), dtype=torch.uint8, device=d) for _ in range(2)]
+        self.mask = [torch.empty((b, n + 1), dtype=torch.bool, device=d) for _ in range(2)]
+        self.done = torch.empty(b, dtype=torch.bool, device=d)
+        self.step_reward = torch.empty(b, dtype=torch.bool, device=d)
+        self.not_done = torch.empty(T, dtype=torch.int32, device=d)
+        self.reward = torch.empty(b, dtype=torch.float32, device=d)
+        self.status = torch.zeros(1, dtype=torch.int32, device=d)
+        self.stream = torch.cuda.Stream(d)
+        self.graphs = None
+        self.T = None
+
+    def _reset(self, s):
+        nat.call("co_cvrp_reset", self.b, self.n, nat.ptr(self.depot), nat.ptr(self.locs_in),
+                 nat.ptr(self.demand), self.vcap, nat.ptr(self.locs), nat.ptr(self.cur[0]),
+                 nat.ptr(self.used[0]), nat.ptr(self.vcap_t), nat.ptr(self.visited[0]),
+                 nat.ptr(self.mask[0]), s)
+
+    def _step(self, t, s):
+        k, k1 = t % 2, (t + 1) % 2
+        nat.call("co_cvrp_nearest_action", self.b, self.n, nat.ptr(self.locs),
+                 nat.ptr(self.mask[k]), nat.ptr(self.cur[t]), nat.ptr(self.acts[t]), s)
+        nat.call("co_cvrp_step", self.b, self.n, nat.ptr(self.acts[t]), nat.ptr(self.demand),
+                 nat.ptr(self.used[t]), nat.ptr(self.used[t + 1]), nat.ptr(self.vcap_t),
+                 nat.ptr(self.visited[k]), nat.ptr(self.visited[k1]), nat.ptr(self.cur[t + 1]),
+                 nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.mask[k1]),
+                 nat.ptr(self.status), s)
+        nat.call("co_count_not_done", nat.ptr(self.done), self.b, nat.ptr(self.not_done[t:]), s)
+
+    def _ranges(self):
+        first = min(self.n, self.max_steps)
+        out = [(0, first)]
+        t = first
+        while t < self.max_steps:
+            out.append((t, min(t + self.chunk, self.max_steps)))
+            t += self.chunk
+        return out
+
+    def capture(self):
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.stream(self.stream):  # warm-up: load code objects
+            self._reset(self.stream.cuda_stream)
+            self._step(0, self.stream.cuda_stream)
+        self.stream.synchronize()
+        self.graphs = []
+        for j, (t0, t1) in enumerate(self._ranges()):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream):
+                s = torch.cuda.current_stream(self.device).cuda_stream
+                if j == 0:
+                    self._reset(s)
+                for t in range(t0, t1):
+                    self._step(t, s)
+            self.graphs.append((t0, t1, g))
+        return self
+
+    def replay(self):
+        """One episode; returns the episode length T (host sync once per chunk)."""
+        if self.graphs is None:
+            self.capture()
+        self.T = None
+        for t0, t1, g in self.graphs:
+            g.replay()
+            if t1 >= self.n and int(self.not_done[t1 - 1].item()) == 0:
+                nd = self.not_done[t0:t1].cpu()
+                self.T = t0 + int((nd == 0).nonzero()[0, 0]) + 1
+                break
+        if self.T is None:
+            raise RuntimeError(f"CVRP rollout: not done after {self.max_steps} steps")
+        acts = self.acts[:self.T]
+        nat.call("co_cvrp_reward", self.b, self.n, self.T, nat.ptr(self.locs), nat.ptr(acts), 1,
+                 self.b, nat.ptr(self.demand), nat.ptr(self.vcap_t), 1, nat.ptr(self.reward),
+                 nat.ptr(self.status), torch.cuda.current_stream(self.device).cuda_stream)
+        return self.T
+
+    def final_state(self):
+        T = self.T
+        return {"locs": self.locs, "current_node": self.cur[T].view(self.b, 1),
+                "used_capacity": self.used[T].view(self.b, 1),
+                "vehicle_capacity": self.vcap_t, "visited": self.visited[T % 2],
+                "action_mask": self.mask[T % 2], "done": self.done, "reward": self.reward,
+                "actions": self.acts[:T].t(), "steps": T}

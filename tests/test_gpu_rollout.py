@@ -130,3 +130,66 @@ def test_slap_rollout_matches_oracle(dev, cls_name, b, policy):
     assert torch.equal(st["actions"].cpu(), a)
     got = st["reward"].cpu()
     assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
+
+
+# --------------------------------------------------------------------------- CVRP
+def _cvrp_ref(b, n, seed):
+    from oracle.envs import CVRPOracle, cvrp_nearest_action
+    from oracle.td import TD
+
+    env = CVRPOracle(num_loc=n, seed=seed)
+    gen = env.generate([b])
+    td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    r, tdf, a = ref_rollout(env, td, cvrp_nearest_action)
+    return gen, float(env.vehicle_capacity), a, r, tdf
+
+
+def _check_cvrp(state, a, r, tdf):
+    assert state["steps"] == a.shape[1]
+    assert torch.equal(state["actions"].cpu(), a)
+    for k in ("locs", "visited", "action_mask", "vehicle_capacity"):
+        assert torch.equal(state[k].cpu(), tdf[k].to(state[k].dtype)), k
+    assert torch.equal(state["current_node"].cpu(), tdf["current_node"].view(-1, 1))
+    assert torch.equal(state["used_capacity"].cpu(), tdf["used_capacity"].view(-1, 1))
+    assert torch.equal(state["done"].cpu(), tdf["done"].view(-1))
+    got = state["reward"].cpu()
+    assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
+
+
+@pytest.mark.parametrize("b,n", [(1, 5), (64, 20), (256, 100), (33, 63), (17, 130)])
+@pytest.mark.parametrize("kind", ["fused", "stepwise"])
+def test_cvrp_rollout_matches_oracle(dev, b, n, kind):
+    from rl4co_slap_amd.rollout.engine import CVRPFusedEpisode, CVRPStepwiseEpisode
+
+    gen, vcap, a, r, tdf = _cvrp_ref(b, n, 4321 + n)
+    td = {k: v.to(dev) for k, v in gen.items()}
+    if kind == "fused":
+        ep = CVRPFusedEpisode(td, vehicle_capacity=vcap)
+        ep.run_eager()
+        torch.cuda.synchronize()
+        assert int(ep.status.item()) == 0
+        _check_cvrp(ep.final_state(), a, r, tdf)
+        ep.capture()
+        ep.replay()
+        torch.cuda.synchronize()
+        _check_cvrp(ep.final_state(), a, r, tdf)
+    else:
+        ep = CVRPStepwiseEpisode(td, vehicle_capacity=vcap, chunk=4).capture()
+        for _ in range(2):  # replays are repeatable
+            T = ep.replay()
+            torch.cuda.synchronize()
+            assert T == a.shape[1]
+            assert int(ep.status.item()) == 0
+            _check_cvrp(ep.final_state(), a, r, tdf)
+
+
+def test_cvrp_fused_truncation_flag(dev):
+    from rl4co_slap_amd.rollout.engine import CVRPFusedEpisode
+
+    gen, vcap, a, r, tdf = _cvrp_ref(8, 20, 5)
+    ep = CVRPFusedEpisode({k: v.to(dev) for k, v in gen.items()}, vehicle_capacity=vcap,
+                          max_steps=10)
+    ep.run_eager()
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="not done"):
+        ep.final_state()
