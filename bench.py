@@ -193,7 +193,7 @@ def main():
     achieved = bytes_per_launch / per_launch / 1e9
     traffic, traffic_src = (None, None)
     if (b, n) == (65536, 100):
-        traffic, traffic_src = pmc_traffic("tsp_fused_teacher", "tsp_rollout_kernel<2, false, true>")
+        traffic, traffic_src = pmc_traffic("tsp_fused_teacher", "tsp_teacher_kernel<2, 4, true>")
 
     out = {
         "metric": "env-steps/sec (batch×decode) SLAP & TSP-100 at 1/2/4/8 MI355X",
@@ -205,7 +205,7 @@ def main():
                                "reward + validity) as one fused launch (co_tsp_rollout)",
                    "batch_per_gpu": b, "num_loc": n, "env_steps_per_episode": n,
                    "parallelism": f"dp{world}: disjoint instance shards, no data-path collective"},
-        "roofline": {"bound": "hbm", "kernel": "tsp_rollout_kernel<2,false> (co_tsp_rollout)",
+        "roofline": {"bound": "hbm", "kernel": "tsp_teacher_kernel<2,4,true> (co_tsp_rollout)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,

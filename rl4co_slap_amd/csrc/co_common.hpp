@@ -198,8 +198,8 @@ inline int launch_status() {
 
 // internal (not part of the public C ABI): rollout.hip's thread-per-instance reward
 int co_internal_tsp_reward_stepmajor(int64_t B, int64_t N, const float* locs,
-                                     const int64_t* acts, int64_t st, int check, float* reward,
-                                     int32_t* status, void* stream);
+                                     int64_t locs_batch, const int64_t* acts, int64_t st,
+                                     int check, float* reward, int32_t* status, void* stream);
 // internal: nearest.hip's register-resident nearest-policy TSP episode
 int co_internal_tsp_nearest_rollout(int64_t B, int64_t N, const float* locs, int64_t* acts_out,
                                     uint8_t* mask_out, int64_t* first_out, int64_t* cur_out,

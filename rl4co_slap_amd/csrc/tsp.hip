@@ -189,10 +189,10 @@ extern "C" int co_tsp_reward(int64_t B, int64_t N, int64_t T, const float* locs,
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
   // step-major actions ([T, B], the stepwise engine's layout): thread per instance,
   // coalesced [B]-row loads, LDS-staged coordinates (rollout.hip)
-  if (sb == 1 && st == B && T == N && N <= 256 && B > 1 && locs_batch == B &&
-      (reinterpret_cast<uintptr_t>(locs) & 15) == 0)
-    return co_internal_tsp_reward_stepmajor(B, N, locs, actions, st, check, reward, status,
-                                            stream);
+  if (sb == 1 && st == B && T == N && N <= 256 && B > 1 &&
+      (locs_batch == B || locs_batch % 64 == 0) && (reinterpret_cast<uintptr_t>(locs) & 15) == 0)
+    return co_internal_tsp_reward_stepmajor(B, N, locs, locs_batch, actions, st, check, reward,
+                                            status, stream);
   const size_t words = (size_t)((T + 31) / 32);
   constexpr int W = 4;
   const size_t shmem = check ? W * words * sizeof(uint32_t) : 0;

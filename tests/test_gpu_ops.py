@@ -131,3 +131,31 @@ def test_decode_sampling_distribution(dev):
     assert torch.equal(act, act2.cpu())
     lp_ref = odec.process_logits(logits, mask).gather(1, act[:, None]).squeeze(1)
     assert (lp.cpu() - lp_ref).abs().max() < 2e-6
+
+
+@pytest.mark.parametrize("lb,s,n", [(64, 3, 20), (128, 2, 100), (192, 1, 64)])
+def test_tsp_reward_stepmajor_shared_locs(dev, lb, s, n):
+    """co_tsp_reward on step-major actions [N, S*LB] with env e on coordinate row e % LB
+    (the POMO layout): the thread-per-instance path, checked against the oracle's
+    get_tour_length; a duplicated node sets the invalid-tour flag."""
+    from oracle.ops import get_tour_length as ref_len
+    from rl4co_slap_amd import _native as nat
+
+    g = torch.Generator().manual_seed(lb + n)
+    locs = torch.rand(lb, n, 2, generator=g)
+    e = s * lb
+    acts = torch.rand(e, n, generator=g).argsort(1)
+    want = -ref_len(locs.repeat(s, 1, 1).gather(1, acts[..., None].expand(e, n, 2)))
+    ld, ad = locs.to(dev), acts.t().contiguous().to(dev)
+    out = torch.empty(e, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    nat.call("co_tsp_reward", e, n, n, nat.ptr(ld), lb, nat.ptr(ad), 1, e, 1, nat.ptr(out),
+             nat.ptr(st), nat.stream_of(out))
+    torch.cuda.synchronize()
+    assert int(st.item()) == 0
+    assert ((out.cpu() - want).abs() <= 1e-5 * want.abs().clamp(min=1)).all()
+    ad[3, e - 1] = ad[4, e - 1]  # not a permutation any more
+    nat.call("co_tsp_reward", e, n, n, nat.ptr(ld), lb, nat.ptr(ad), 1, e, 1, nat.ptr(out),
+             nat.ptr(st), nat.stream_of(out))
+    torch.cuda.synchronize()
+    assert int(st.item()) & nat.ST_INVALID_TOUR

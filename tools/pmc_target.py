@@ -28,6 +28,21 @@ if args.kernel.startswith("tsp"):
         ep = engine.TSPFusedEpisode(locs.to(dev), None, policy="nearest")
     else:
         ep = engine.TSPStepwiseEpisode(locs.to(dev), acts.to(dev))
+elif args.kernel == "cvrp_fused_nearest":
+    torch.manual_seed(1234)
+    locs_all = torch.rand(32768, 101, 2)
+    demand = ((torch.rand(32768, 100) * 9).int() + 1).float() / 50.0
+    ep = engine.CVRPFusedEpisode({"depot": locs_all[:, 0].contiguous().to(dev),
+                                  "locs": locs_all[:, 1:].contiguous().to(dev),
+                                  "demand": demand.to(dev)})
+elif args.kernel == "pomo_tsp100":
+    from rl4co_slap_amd.rollout.pomo import POMOEpisode
+
+    torch.manual_seed(1234)
+    locs = torch.rand(1024, 100, 2).to(dev)
+    g = torch.Generator(device=dev).manual_seed(99)
+    logits = torch.randn((99, 102400, 100), generator=g, device=dev)
+    ep = POMOEpisode(locs, logits, tanh_clipping=10.0)
 else:
     import numpy as np
 
