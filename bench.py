@@ -153,6 +153,35 @@ def cpu_baseline_slap(b=2048, episodes=2):
                       f"slap/env.py:61-62 kept), B={b}, median of {episodes}"}
 
 
+def cpu_baseline_cvrp(b=16384, n=100, episodes=2):
+    """The oracle's CVRP-100 rollout with the nearest-feasible policy (config 3 recipe,
+    smaller B), including get_reward's Python capacity loop."""
+    from oracle.envs import CVRPOracle, cvrp_nearest_action
+    from oracle.rollout import rollout
+    from oracle.td import TD
+
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    torch.manual_seed(1234)
+    locs_all = torch.rand(b, n + 1, 2)
+    demand = ((torch.rand(b, n) * 9).int() + 1).float() / 50.0
+    env = CVRPOracle(num_loc=n, seed=1234)
+    times, steps = [], 0
+    for _ in range(episodes + 1):
+        td = env.reset(TD({"depot": locs_all[:, 0].clone(), "locs": locs_all[:, 1:].clone(),
+                           "demand": demand.clone(),
+                           "capacity": torch.full((b, 1), 50.0)}, [b]))
+        t0 = time.perf_counter()
+        _, _, acts = rollout(env, td, cvrp_nearest_action)
+        times.append(time.perf_counter() - t0)
+        steps = acts.shape[1]
+    med = sorted(times[1:])[len(times[1:]) // 2]
+    return {"value": b * steps / med, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle CVRP-{n} rollout, nearest-feasible policy, B={b}, T={steps} "
+                      f"steps, get_reward with the validity + capacity loop, median of "
+                      f"{episodes}"}
+
+
 def pmc_traffic(target, kernel_prefix):
     """HBM bytes per launch measured by rocprofv3 PMC passes (scripts/gpu_pmc.sh ->
     tools/pmc_summarize.py -> profiles/*_pmc_traffic.json, newest round first)."""
@@ -234,6 +263,9 @@ def main():
         del ne
         # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
         modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
+        # the north star's "SLAP at batch 65,536" (fused episode only)
+        modes.update({k2 + "_b65536": v for k2, v in
+                      bench_slap(65536, k, world, rank, dev, stepwise=False).items()})
         # POMO TSP-100 (config 5): 1,024 instances x 100 starts per GPU, decode-fused steps
         # on HBM-resident logits, shared baseline + RCCL all-gather of per-instance results
         modes["pomo_tsp100"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev)
@@ -245,13 +277,14 @@ def main():
         out["cpu_baseline"] = cpu_baseline_tsp(locs_cpu, acts_cpu)
         if not args.no_modes:
             out["cpu_baseline_slap"] = cpu_baseline_slap()
+            out["cpu_baseline_cvrp"] = cpu_baseline_cvrp()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def bench_slap(b, k, world, rank, dev):
+def bench_slap(b, k, world, rank, dev, stepwise=True):
     import numpy as np
 
     from rl4co_slap_amd.envs.slap import SLAPGenerator
@@ -270,7 +303,12 @@ def bench_slap(b, k, world, rank, dev):
     t = max_over_ranks(wall, world, dev)
     out["slap_fused_closest"] = {"value": world * b * 20 * 4 * k / t,
                                  "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
-                                 "launch_us": ev / (4 * k) * 1e6}
+                                 "launch_us": ev / (4 * k) * 1e6,
+                                 "bytes_per_episode": 2834,
+                                 "achieved_GBps": b * 2834 / (ev / (4 * k)) / 1e9}
+    del fu
+    if not stepwise:
+        return out
     ep = SLAPStepwiseEpisode(td, policy="closest").capture()
     wall, ev = timed(ep.replay, k, 2, world, dev)
     t = max_over_ranks(wall, world, dev)
