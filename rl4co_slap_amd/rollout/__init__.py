@@ -1,3 +1,7 @@
-from .engine import SLAPFusedEpisode, SLAPStepwiseEpisode, TSPFusedEpisode, TSPStepwiseEpisode
+from .constructive import ConstructiveDecoder, ConstructivePolicy, LogitsDecoder, NoEncoder
+from .engine import (CVRPFusedEpisode, CVRPStepwiseEpisode, SLAPFusedEpisode,
+                     SLAPStepwiseEpisode, TSPFusedEpisode, TSPStepwiseEpisode)
 
-__all__ = ["TSPStepwiseEpisode", "TSPFusedEpisode", "SLAPStepwiseEpisode", "SLAPFusedEpisode"]
+__all__ = ["TSPStepwiseEpisode", "TSPFusedEpisode", "SLAPStepwiseEpisode", "SLAPFusedEpisode",
+           "CVRPFusedEpisode", "CVRPStepwiseEpisode", "ConstructivePolicy",
+           "ConstructiveDecoder", "LogitsDecoder", "NoEncoder"]

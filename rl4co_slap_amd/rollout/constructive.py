@@ -1,0 +1,132 @@
+"""The constructive decode loop of ``rl4co/models/common/constructive/base.py:158-276``
+(``ConstructivePolicy``) over the MI355X env and decoding kernels.
+
+The encoder / decoder networks are the consumers of this API and stay PyTorch modules
+(or plain callables): ``encoder(td) -> (hidden, init_embeds)`` and ``decoder(td, hidden,
+num_starts) -> (logits, mask)`` with an optional ``decoder.pre_decoder_hook(td, env,
+hidden, num_starts)``.  Everything between them is the hot path: the decoding step
+(``co_decode_step``: tanh clip, mask, temperature, log-softmax, greedy / sampling /
+evaluate selection in one launch), ``env.step`` on the env kernels, the multistart
+hooks and the episode reward.  As in the reference, ``while not td["done"].all()``
+reads the done flags once per step.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Callable, Optional, Union
+
+import torch
+from torch import nn
+
+from ..envs import get_env
+from ..envs.base import RL4COEnvBase
+from ..utils.decoding import get_decoding_strategy, get_log_likelihood
+from ..utils.ops import calculate_entropy
+
+log = logging.getLogger(__name__)
+
+
+class NoEncoder(nn.Module):
+    """``constructive/base.py:36-40``: no encoder, hidden = initial embeddings = None."""
+
+    def forward(self, td):
+        return None, None
+
+
+class ConstructiveDecoder(nn.Module):
+    """``constructive/base.py:43-86`` interface: ``forward(td, hidden, num_starts)``
+    returns ``(logits, mask)``; ``pre_decoder_hook`` passes through by default."""
+
+    def forward(self, td, hidden=None, num_starts: int = 0):
+        raise NotImplementedError
+
+    def pre_decoder_hook(self, td, env, hidden=None, num_starts: int = 0):
+        return td, env, hidden
+
+
+class LogitsDecoder(ConstructiveDecoder):
+    """Adapter for a plain ``logits_fn(td) -> logits [B, n_actions]`` (the mask is the
+    env's ``action_mask``), e.g. a heuristic or a network head evaluated elsewhere."""
+
+    def __init__(self, logits_fn: Callable):
+        super().__init__()
+        self.logits_fn = logits_fn
+
+    def forward(self, td, hidden=None, num_starts: int = 0):
+        return self.logits_fn(td), td["action_mask"]
+
+
+class ConstructivePolicy(nn.Module):
+    """``constructive/base.py:88-276``: same constructor and ``forward`` arguments."""
+
+    def __init__(self, encoder: Union[nn.Module, Callable, None],
+                 decoder: Union[nn.Module, Callable], env_name: str = "tsp",
+                 temperature: float = 1.0, tanh_clipping: float = 0, mask_logits: bool = True,
+                 train_decode_type: str = "sampling", val_decode_type: str = "greedy",
+                 test_decode_type: str = "greedy", **unused_kw):
+        super().__init__()
+        if len(unused_kw) > 0:
+            log.error(f"Found {len(unused_kw)} unused kwargs: {unused_kw}")
+        self.env_name = env_name
+        if encoder is None:
+            log.warning("`None` was provided as encoder. Using `NoEncoder`.")
+            encoder = NoEncoder()
+        self.encoder = encoder
+        self.decoder = decoder
+        self.temperature, self.tanh_clipping = temperature, tanh_clipping
+        self.mask_logits = mask_logits
+        self.train_decode_type = train_decode_type
+        self.val_decode_type = val_decode_type
+        self.test_decode_type = test_decode_type
+
+    def forward(self, td, env: Optional[Union[str, RL4COEnvBase]] = None, phase: str = "train",
+                calc_reward: bool = True, return_actions: bool = False,
+                return_entropy: bool = False, return_hidden: bool = False,
+                return_init_embeds: bool = False, return_sum_log_likelihood: bool = True,
+                actions=None, max_steps=1_000_000, **decoding_kwargs) -> dict:
+        hidden, init_embeds = self.encoder(td)
+        if isinstance(env, str) or env is None:
+            env_name = self.env_name if env is None else env
+            log.info(f"Instantiated environment not provided; instantiating {env_name}")
+            env = get_env(env_name, device=td.device)
+        decode_type = decoding_kwargs.pop("decode_type", None)
+        if actions is not None:
+            decode_type = "evaluate"
+        elif decode_type is None:
+            decode_type = getattr(self, f"{phase}_decode_type")
+        strategy = get_decoding_strategy(
+            decode_type,
+            temperature=decoding_kwargs.pop("temperature", self.temperature),
+            tanh_clipping=decoding_kwargs.pop("tanh_clipping", self.tanh_clipping),
+            mask_logits=decoding_kwargs.pop("mask_logits", self.mask_logits),
+            store_all_logp=decoding_kwargs.pop("store_all_logp", return_entropy),
+            **decoding_kwargs)
+        td, env, num_starts = strategy.pre_decoder_hook(td, env)
+        hook = getattr(self.decoder, "pre_decoder_hook", None)
+        if hook is not None:
+            td, env, hidden = hook(td, env, hidden, num_starts)
+        step = 0
+        while not td["done"].all():
+            logits, mask = self.decoder(td, hidden, num_starts)
+            td = strategy.step(logits, mask, td,
+                               action=actions[..., step] if actions is not None else None)
+            td = env.step(td)["next"]
+            step += 1
+            if step > max_steps:
+                log.error(f"Exceeded maximum number of steps ({max_steps}) duing decoding")
+                break
+        logprobs, actions, td, env = strategy.post_decoder_hook(td, env)
+        if calc_reward:
+            td.set("reward", env.get_reward(td, actions))
+        out = {"reward": td["reward"],
+               "log_likelihood": get_log_likelihood(logprobs, actions, td.get("mask", None),
+                                                    return_sum_log_likelihood)}
+        if return_actions:
+            out["actions"] = actions
+        if return_entropy:
+            out["entropy"] = calculate_entropy(logprobs)
+        if return_hidden:
+            out["hidden"] = hidden
+        if return_init_embeds:
+            out["init_embeds"] = init_embeds
+        return out

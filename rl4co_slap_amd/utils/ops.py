@@ -146,3 +146,13 @@ def get_best_actions(actions, max_idxs):
     """``ops.py:186-188``."""
     actions = unbatchify(actions, max_idxs.shape[0])
     return actions.gather(0, max_idxs[..., None, None])
+
+
+def calculate_entropy(logprobs: Tensor):
+    """``ops.py:114-122``: entropy of per-step log-probabilities ``[B, steps, n]``,
+    summed over steps (torch ops on the device tensors; not on the timed path)."""
+    logprobs = torch.nan_to_num(logprobs, nan=0.0)
+    entropy = -(logprobs.exp() * logprobs).sum(dim=-1)
+    entropy = entropy.sum(dim=1)
+    assert entropy.isfinite().all(), "Entropy is not finite"
+    return entropy
