@@ -70,6 +70,14 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
+def sum_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
 def timed(run, steps, warmup, world, dev):
     """W untimed runs, then exactly K timed runs bracketed by barrier + synchronize.
     Returns (wall seconds, HIP-event seconds on the launching stream)."""
@@ -335,7 +343,8 @@ def bench_cvrp(b, n, k, world, rank, dev):
     st = fu.final_state()
     T = st["steps"]
     t = max_over_ranks(wall, world, dev)
-    out["cvrp_fused_nearest"] = {"value": world * b * T * 4 * k / t,
+    steps_all = sum_over_ranks(b * T, world, dev)  # T differs per rank (own instances)
+    out["cvrp_fused_nearest"] = {"value": steps_all * 4 * k / t,
                                  "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
                                  "num_loc": n, "episode_steps": T,
                                  "launch_us": ev / (4 * k) * 1e6}
@@ -343,7 +352,7 @@ def bench_cvrp(b, n, k, world, rank, dev):
     wall, ev = timed(sw.replay, k, 1, world, dev)
     t = max_over_ranks(wall, world, dev)
     assert sw.T == T
-    out["cvrp_stepwise_graph"] = {"value": world * b * T * k / t, "ms_per_episode": t / k * 1e3,
+    out["cvrp_stepwise_graph"] = {"value": steps_all * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "episode_steps": T,
                                   "bytes_per_env_step": 7 * n + 33}
     return out
