@@ -126,7 +126,7 @@ struct DecodeRow {
         v = x[k];
         if (clip > 0.f) v = tanhf(v) * clip;
         if (!mk[k]) v = NEG_INF;
-        v = v / temp;
+        if (temp != 1.f) v = v / temp;  // x / 1 == x exactly: skip the IEEE divide
         m = fmaxf(m, v);
       }
       x[k] = v;
