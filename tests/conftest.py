@@ -29,5 +29,7 @@ def dev():
 
     from rl4co_slap_amd import _native
 
+    if os.environ.get("CO_TEST_LIB"):  # a tuning variant (tools/build_variants.sh)
+        _native.LIB_PATH = os.environ["CO_TEST_LIB"]
     _native.load()  # fail loudly if the library is missing
     return torch.device("cuda:0")
