@@ -267,6 +267,18 @@ int co_pomo_shared_baseline(int64_t instances, int64_t starts, const float* rewa
                             const float* log_likelihood, float* bl, float* max_reward,
                             int64_t* best_start, float* adv, float* loss_terms, void* stream);
 
+/* dihedral_8_augmentation (rl4co/data/transforms.py:15-37): out[8B, N, 2], row r*B + b
+ * = transform r of instance b, r in the reference's order (x,y) (1-x,y) (x,1-y)
+ * (1-x,1-y) (y,x) (1-y,x) (y,1-x) (1-y,1-x). */
+int co_dihedral8_augment(int64_t batch, int64_t num_loc, const float* xy, float* out,
+                         void* stream);
+
+/* symmetric_transform (rl4co/data/transforms.py:49-71) given the per-row angles phi[B]
+ * (drawn by the caller exactly as symmetric_augmentation does, transforms.py:74-93):
+ * rotate (x,y) - offset by phi, swap the axes where phi > 2*pi, add the offset. */
+int co_symmetric_augment(int64_t batch, int64_t num_loc, const float* xy, const float* phi,
+                         float offset, float* out, void* stream);
+
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 

@@ -47,6 +47,8 @@ _SIGS = {
     "co_tsp_rollout": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
     "co_slap_rollout": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                         _p, _p, _p, _p],
+    "co_dihedral8_augment": [_i64, _i64, _p, _p, _p],
+    "co_symmetric_augment": [_i64, _i64, _p, _p, _f32, _p, _p],
     "co_cvrp_rollout": [_i64, _i64, _p, _p, _p, _f32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                         _p, _p, _p, _p, _p],
 }

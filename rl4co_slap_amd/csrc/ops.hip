@@ -159,3 +159,71 @@ extern "C" int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count,
                      (hipStream_t)stream, done, n, count);
   return launch_status();
 }
+
+// ------------------------------------------------------------------ augmentation
+// data/transforms.py:15-37 dihedral_8_augmentation: out[r*B*N + i] = transform r of
+// in[i] (i = b*N + c), r = 0..7 in the reference's order z0..z7; the [8B, N, 2] output is
+// the batchify layout (row r*B + b).  1 - x in f32, exactly as the reference.
+namespace {
+__global__ __launch_bounds__(256) void dihedral8_kernel(int64_t BN, const float2* __restrict__ in,
+                                                        float2* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < BN;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float2 p = in[i];
+    const float x = p.x, y = p.y, nx = 1.f - x, ny = 1.f - y;
+    out[i] = make_float2(x, y);
+    out[BN + i] = make_float2(nx, y);
+    out[2 * BN + i] = make_float2(x, ny);
+    out[3 * BN + i] = make_float2(nx, ny);
+    out[4 * BN + i] = make_float2(y, x);
+    out[5 * BN + i] = make_float2(ny, x);
+    out[6 * BN + i] = make_float2(y, nx);
+    out[7 * BN + i] = make_float2(ny, nx);
+  }
+}
+
+// data/transforms.py:49-71 symmetric_transform: per row b, rotate (x, y) - offset by
+// phi[b], swap the axes when phi[b] > 2*pi (f32 compare), add the offset back.  f32
+// separately rounded products as ATen evaluates them (-ffp-contract=off).
+__global__ __launch_bounds__(256) void symmetric_kernel(int64_t B, int64_t N,
+                                                        const float2* __restrict__ in,
+                                                        const float* __restrict__ phi,
+                                                        float offset, float2* __restrict__ out) {
+  const float two_pi = (float)(2.0 * 3.14159265358979323846);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < B * N;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float f = phi[i / N];
+    const float c = cosf(f), s = sinf(f);
+    const float2 p = in[i];
+    const float x = p.x - offset, y = p.y - offset;
+    const float xp = c * x - s * y, yp = s * x + c * y;
+    const bool flip = f > two_pi;
+    out[i] = make_float2((flip ? yp : xp) + offset, (flip ? xp : yp) + offset);
+  }
+}
+}  // namespace
+
+extern "C" int co_dihedral8_augment(int64_t B, int64_t N, const float* xy, float* out,
+                                    void* stream) {
+  if (B < 0 || N <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!xy || !out) return CO_E_INVAL;
+  if ((reinterpret_cast<uintptr_t>(xy) | reinterpret_cast<uintptr_t>(out)) & 7) return CO_E_ALIGN;
+  const int64_t bn = B * N;
+  hipLaunchKernelGGL(dihedral8_kernel, dim3(grid_for(bn, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, bn, reinterpret_cast<const float2*>(xy),
+                     reinterpret_cast<float2*>(out));
+  return launch_status();
+}
+
+extern "C" int co_symmetric_augment(int64_t B, int64_t N, const float* xy, const float* phi,
+                                    float offset, float* out, void* stream) {
+  if (B < 0 || N <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!xy || !phi || !out) return CO_E_INVAL;
+  if ((reinterpret_cast<uintptr_t>(xy) | reinterpret_cast<uintptr_t>(out)) & 7) return CO_E_ALIGN;
+  hipLaunchKernelGGL(symmetric_kernel, dim3(grid_for(B * N, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, B, N, reinterpret_cast<const float2*>(xy), phi, offset,
+                     reinterpret_cast<float2*>(out));
+  return launch_status();
+}
