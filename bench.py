@@ -279,6 +279,9 @@ def main():
         modes["pomo_tsp100"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev)
         # CVRP-100 (config 3), nearest-feasible policy: fused episode and stepwise loop
         modes.update(bench_cvrp(32768, 100, k, world, rank, dev))
+        # instance generation, timed separately (SURVEY.md 8d protocol; 8f rank 1)
+        modes["slap_generate_b16384"] = bench_generate_slap(args.slap_batch, dev,
+                                                            with_ref=(rank == 0 and world == 1))
         out["modes"] = modes
 
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -355,6 +358,36 @@ def bench_cvrp(b, n, k, world, rank, dev):
     out["cvrp_stepwise_graph"] = {"value": steps_all * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "episode_steps": T,
                                   "bytes_per_env_step": 7 * n + 33}
+    return out
+
+
+def bench_generate_slap(b, dev, reps=3, with_ref=True):
+    """SLAP instance generation incl. the [B, 100, 100] dist_mat: co_slap_generate on the
+    device vs the host generator (vectorised) + copy; the oracle's restatement of the
+    reference's B x L Python loop is timed on a small sample and scaled per instance."""
+    from rl4co_slap_amd.envs.slap import SLAPGenerator
+
+    gd, gh = SLAPGenerator(device=dev), SLAPGenerator()
+    gd(b)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gd(b)
+    torch.cuda.synchronize(dev)
+    t_dev = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    gh(b).to(dev)
+    torch.cuda.synchronize(dev)
+    t_host = time.perf_counter() - t0
+    out = {"device_ms": t_dev * 1e3, "host_vectorised_plus_copy_ms": t_host * 1e3,
+           "dist_mat_MB": b * 100 * 100 * 4 / 1e6}
+    if with_ref:
+        from oracle.envs import SLAPOracle
+
+        nb = 64
+        t0 = time.perf_counter()
+        SLAPOracle(seed=1).generate([nb])
+        out["reference_loop_ms_scaled"] = (time.perf_counter() - t0) / nb * b * 1e3
     return out
 
 

@@ -267,6 +267,16 @@ int co_pomo_shared_baseline(int64_t instances, int64_t starts, const float* rewa
                             const float* log_likelihood, float* bl, float* max_reward,
                             int64_t* best_start, float* adv, float* loss_terms, void* stream);
 
+/* The deterministic part of SLAPGenerator._generate (slap/generator.py:51-81,137-155):
+ * locs[B,L,2] aisle grid (x = aisle * inter_aisle_dist, y = loc * inter_loc_dist, products
+ * in double rounded to f32), depot_loc_dist[B,L] and dist_mat[B,L,L] (nullable;
+ * Manhattan, f32) and assignment[B,P] = -1 (nullable); L = n_aisles * n_locs.  freq and
+ * the picklists stay on the host RNG streams. */
+int co_slap_generate(int64_t batch, int64_t n_aisles, int64_t n_locs, double inter_aisle_dist,
+                     double inter_loc_dist, int64_t n_products, float* locs,
+                     float* depot_loc_dist, float* dist_mat, int32_t* assignment,
+                     void* stream);
+
 /* dihedral_8_augmentation (rl4co/data/transforms.py:15-37): out[8B, N, 2], row r*B + b
  * = transform r of instance b, r in the reference's order (x,y) (1-x,y) (x,1-y)
  * (1-x,1-y) (y,x) (1-y,x) (y,1-x) (1-y,1-x). */

@@ -20,6 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libco_env.so")
 
 _i64, _i32, _f32, _u64, _p = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
+_f64 = ctypes.c_double
 
 # name -> argtypes (all return int status)
 _SIGS = {
@@ -48,6 +49,7 @@ _SIGS = {
     "co_slap_rollout": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                         _p, _p, _p, _p],
     "co_dihedral8_augment": [_i64, _i64, _p, _p, _p],
+    "co_slap_generate": [_i64, _i64, _i64, _f64, _f64, _i64, _p, _p, _p, _p, _p],
     "co_symmetric_augment": [_i64, _i64, _p, _p, _f32, _p, _p],
     "co_cvrp_rollout": [_i64, _i64, _p, _p, _p, _f32, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                         _p, _p, _p, _p, _p],

@@ -225,3 +225,86 @@ extern "C" int co_slap_closest_free_action(int64_t B, int64_t L, const float* di
                      (hipStream_t)stream, B, (int)L, dist, mask, out);
   return launch_status();
 }
+
+// ---------------------------------------------------------------- instance generator
+// The deterministic part of SLAPGenerator._generate (slap/generator.py:51-81,137-155) on
+// the device: aisle-grid coordinates x = aisle * inter_aisle_dist, y = loc *
+// inter_loc_dist (python float products rounded to f32), the Manhattan matrix
+// |dx| + |dy| in f32 (one rounding, as torch.sum over the size-2 dim), its depot row, and
+// the -1 assignment.  freq and picklist come from the host RNG streams.
+namespace {
+__device__ __forceinline__ float2 slap_xy(int i, int n_locs, double inter_aisle,
+                                          double inter_loc) {
+  return make_float2((float)((double)(i / n_locs) * inter_aisle),
+                     (float)((double)(i % n_locs) * inter_loc));
+}
+
+__global__ __launch_bounds__(256) void slap_gen_rows_kernel(int64_t B, int L, int P, int n_locs,
+                                                            double inter_aisle, double inter_loc,
+                                                            float2* __restrict__ locs,
+                                                            float* __restrict__ depot,
+                                                            int32_t* __restrict__ assign) {
+  const float2 p0 = slap_xy(0, n_locs, inter_aisle, inter_loc);
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < B * L;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const float2 q = slap_xy((int)(k % L), n_locs, inter_aisle, inter_loc);
+    locs[k] = q;
+    depot[k] = fabsf(p0.x - q.x) + fabsf(p0.y - q.y);
+  }
+  if (assign)
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < B * P;
+         k += (int64_t)gridDim.x * blockDim.x)
+      assign[k] = -1;
+}
+
+// dist_mat[b, i, j]: every instance has the same grid; 4 consecutive j per thread
+// (float4 stores when L % 4 == 0).
+__global__ __launch_bounds__(256) void slap_gen_dist_kernel(int64_t B, int L, int n_locs,
+                                                            double inter_aisle, double inter_loc,
+                                                            float* __restrict__ dist) {
+  const int64_t LL = (int64_t)L * L;
+  const bool vec = (L & 3) == 0;
+  const int64_t units = vec ? B * (LL / 4) : B * LL;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    if (vec) {
+      const int64_t e = u * 4, r = e % LL;
+      const int i = (int)(r / L), j = (int)(r % L);
+      const float2 p = slap_xy(i, n_locs, inter_aisle, inter_loc);
+      float d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float2 o = slap_xy(j + q, n_locs, inter_aisle, inter_loc);
+        d[q] = fabsf(p.x - o.x) + fabsf(p.y - o.y);
+      }
+      *reinterpret_cast<float4*>(dist + e) = make_float4(d[0], d[1], d[2], d[3]);
+    } else {
+      const int64_t r = u % LL;
+      const float2 p = slap_xy((int)(r / L), n_locs, inter_aisle, inter_loc);
+      const float2 o = slap_xy((int)(r % L), n_locs, inter_aisle, inter_loc);
+      dist[u] = fabsf(p.x - o.x) + fabsf(p.y - o.y);
+    }
+  }
+}
+}  // namespace
+
+extern "C" int co_slap_generate(int64_t B, int64_t n_aisles, int64_t n_locs,
+                                double inter_aisle_dist, double inter_loc_dist,
+                                int64_t n_products, float* locs, float* depot_loc_dist,
+                                float* dist_mat, int32_t* assignment, void* stream) {
+  if (B < 0 || n_aisles <= 0 || n_locs <= 0 || n_products < 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!locs || !depot_loc_dist) return CO_E_INVAL;
+  if ((reinterpret_cast<uintptr_t>(locs) & 7) || (reinterpret_cast<uintptr_t>(dist_mat) & 15))
+    return CO_E_ALIGN;
+  const int L = (int)(n_aisles * n_locs);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(slap_gen_rows_kernel, dim3(grid_for(B * L, 256, 8192)), dim3(256), 0, s, B,
+                     L, (int)n_products, (int)n_locs, inter_aisle_dist, inter_loc_dist,
+                     reinterpret_cast<float2*>(locs), depot_loc_dist, assignment);
+  if (dist_mat)
+    hipLaunchKernelGGL(slap_gen_dist_kernel, dim3(grid_for(B * L * L / 4 + 1, 256, 16384)),
+                       dim3(256), 0, s, B, L, (int)n_locs, inter_aisle_dist, inter_loc_dist,
+                       dist_mat);
+  return launch_status();
+}

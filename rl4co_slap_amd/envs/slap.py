@@ -27,13 +27,17 @@ class SLAPGenerator(Generator):
     def __init__(self, n_products: int = 20, n_aisles: int = 10, n_locs: int = 10,
                  inter_loc_dist: float = 1, inter_aisle_dist: float = 2.4, min_freq: int = 1,
                  max_freq: int = 20, max_orders: int = 20, max_products_in_order: int = 5,
-                 materialize_dist_mat: bool = True):
+                 materialize_dist_mat: bool = True, device=None):
         self.n_products, self.n_aisles, self.n_locs = n_products, n_aisles, n_locs
         self.max_orders, self.max_products_in_order = max_orders, max_products_in_order
         self.inter_loc_dist, self.inter_aisle_dist = inter_loc_dist, inter_aisle_dist
         self.min_freq, self.max_freq = min_freq, max_freq
         self.freq_sampler = torch.distributions.Uniform(low=min_freq, high=max_freq)
         self.materialize_dist_mat = materialize_dist_mat
+        # device generation: the deterministic columns (grid, distance
+        # matrices, assignment) are written by co_slap_generate on the device; freq and the
+        # picklists keep the host RNG streams and are copied (1.3 + 13 MB at B = 16,384)
+        self.device = None if device is None else torch.device(device)
 
     @staticmethod
     def _get_distance_matrix(locs: torch.Tensor):
@@ -50,6 +54,8 @@ class SLAPGenerator(Generator):
         return torch.tensor(xy, dtype=torch.float64).to(torch.float32)
 
     def _generate(self, batch_size) -> TensorDict:
+        if self.device is not None and self.device.type == "cuda":
+            return self._generate_device(batch_size)
         freq = self.freq_sampler.sample((*batch_size, self.n_products, 1))
         g = self.grid()
         locs = g.expand(*batch_size, *g.shape).contiguous()
@@ -63,6 +69,26 @@ class SLAPGenerator(Generator):
                 "picklist": picklist, "depot_loc_dist": depot}
         if self.materialize_dist_mat:
             data["dist_mat"] = dist1.expand(*batch_size, *dist1.shape).contiguous()
+        return TensorDict(data, batch_size=batch_size)
+
+    def _generate_device(self, batch_size) -> TensorDict:
+        dev = self.device
+        b, L, P = batch_size[0], self.n_aisles * self.n_locs, self.n_products
+        freq = self.freq_sampler.sample((*batch_size, P, 1))  # same draw order as the host path
+        picklist = torch.from_numpy(np.random.randint(
+            0, P, size=(b, self.max_orders, self.max_products_in_order)).astype(np.int64))
+        locs = torch.empty((b, L, 2), dtype=torch.float32, device=dev)
+        depot = torch.empty((b, L), dtype=torch.float32, device=dev)
+        assign = torch.empty((b, P), dtype=torch.int32, device=dev)
+        dist = (torch.empty((b, L, L), dtype=torch.float32, device=dev)
+                if self.materialize_dist_mat else None)
+        nat.call("co_slap_generate", b, self.n_aisles, self.n_locs, float(self.inter_aisle_dist),
+                 float(self.inter_loc_dist), P, nat.ptr(locs), nat.ptr(depot), nat.ptr(dist),
+                 nat.ptr(assign), nat.stream_of(locs))
+        data = {"freq": freq.to(dev, non_blocking=True), "locs": locs, "assignment": assign,
+                "picklist": picklist.to(dev, non_blocking=True), "depot_loc_dist": depot}
+        if dist is not None:
+            data["dist_mat"] = dist
         return TensorDict(data, batch_size=batch_size)
 
 
