@@ -182,13 +182,16 @@ class TSPFusedEpisode(_GraphEpisode):
         self.reward = torch.empty(b, dtype=torch.float32, device=d)
         self.status = torch.zeros(1, dtype=torch.int32, device=d)
 
-    def _launch(self, s):
         teacher = self.policy == "teacher"
-        nat.call("co_tsp_rollout", self.b, self.n, nat.ptr(self.locs),
-                 nat.ptr(self.acts) if teacher else None, None if teacher else nat.ptr(self.acts),
-                 nat.ptr(self.mask), nat.ptr(self.first), nat.ptr(self.cur), nat.ptr(self.i),
-                 nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.reward),
-                 int(self.check), nat.ptr(self.status), s)
+        self._bound = nat.bind(
+            "co_tsp_rollout", self.b, self.n, nat.ptr(self.locs),
+            nat.ptr(self.acts) if teacher else None, None if teacher else nat.ptr(self.acts),
+            nat.ptr(self.mask), nat.ptr(self.first), nat.ptr(self.cur), nat.ptr(self.i),
+            nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.reward),
+            int(self.check), nat.ptr(self.status))
+
+    def _launch(self, s):
+        self._bound(s)
 
     def final_state(self):
         return {"action_mask": self.mask, "i": self.i, "first_node": self.first,
@@ -226,14 +229,17 @@ class SLAPFusedEpisode(_GraphEpisode):
         self.ratio = torch.empty((b, l), dtype=torch.float32, device=d) if write_ratio else None
         self.status = torch.zeros(1, dtype=torch.int32, device=d)
 
-    def _launch(self, s):
         teacher = self.policy == "teacher"
-        nat.call("co_slap_rollout", self.b, self.l, self.p, self.o, self.k, nat.ptr(self.locs),
-                 nat.ptr(self.picklist), nat.ptr(self.depot_dist), nat.ptr(self.assign0),
-                 nat.ptr(self.acts) if teacher else None, None if teacher else nat.ptr(self.acts),
-                 nat.ptr(self.mask), nat.ptr(self.assign), nat.ptr(self.i), nat.ptr(self.done),
-                 nat.ptr(self.step_reward), nat.ptr(self.reward), nat.ptr(self.ratio),
-                 nat.ptr(self.status), s)
+        self._bound = nat.bind(
+            "co_slap_rollout", self.b, self.l, self.p, self.o, self.k, nat.ptr(self.locs),
+            nat.ptr(self.picklist), nat.ptr(self.depot_dist), nat.ptr(self.assign0),
+            nat.ptr(self.acts) if teacher else None, None if teacher else nat.ptr(self.acts),
+            nat.ptr(self.mask), nat.ptr(self.assign), nat.ptr(self.i), nat.ptr(self.done),
+            nat.ptr(self.step_reward), nat.ptr(self.reward), nat.ptr(self.ratio),
+            nat.ptr(self.status))
+
+    def _launch(self, s):
+        self._bound(s)
 
     def final_state(self):
         return {"action_mask": self.mask, "i": self.i, "assignment": self.assign,
@@ -274,13 +280,16 @@ class CVRPFusedEpisode(_GraphEpisode):
         self.steps = torch.zeros(1, dtype=torch.int32, device=d)
         self.status = torch.zeros(1, dtype=torch.int32, device=d)
 
+        self._bound = nat.bind(
+            "co_cvrp_rollout", self.b, self.n, nat.ptr(self.depot), nat.ptr(self.locs_in),
+            nat.ptr(self.demand), self.vcap, self.max_steps, nat.ptr(self.acts),
+            nat.ptr(self.locs), nat.ptr(self.cur), nat.ptr(self.used), nat.ptr(self.vcap_t),
+            nat.ptr(self.visited), nat.ptr(self.mask), nat.ptr(self.done),
+            nat.ptr(self.step_reward), nat.ptr(self.reward), nat.ptr(self.lens),
+            nat.ptr(self.steps), nat.ptr(self.status))
+
     def _launch(self, s):
-        nat.call("co_cvrp_rollout", self.b, self.n, nat.ptr(self.depot), nat.ptr(self.locs_in),
-                 nat.ptr(self.demand), self.vcap, self.max_steps, nat.ptr(self.acts),
-                 nat.ptr(self.locs), nat.ptr(self.cur), nat.ptr(self.used), nat.ptr(self.vcap_t),
-                 nat.ptr(self.visited), nat.ptr(self.mask), nat.ptr(self.done),
-                 nat.ptr(self.step_reward), nat.ptr(self.reward), nat.ptr(self.lens),
-                 nat.ptr(self.steps), nat.ptr(self.status), s)
+        self._bound(s)
 
     def final_state(self):
         """Post-rollout columns; reads the episode length (one host sync)."""
