@@ -280,15 +280,24 @@ ORACLE_REGISTRY = {"tsp": TSPOracle, "cvrp": CVRPOracle, "slap": SLAPOracle}
 # Cheap deterministic policies used by the env-throughput benchmark
 # (SURVEY section 8d); these define the bench workloads, not reference code.
 # ---------------------------------------------------------------------------
+def _f32_sqrt(sq):
+    """Correctly rounded f32 sqrt (via f64, where double rounding is exact for sqrt).
+    ATen's vectorised CPU sqrt is not correctly rounded in rare cases (e.g. input bits
+    0x3b9f879c: 0x3d8ee5db instead of 0x3d8ee5dc), which would make the bench policies'
+    lowest-index tie rule depend on the CPU's SIMD path."""
+    return torch.sqrt(sq.double()).float()
+
+
 def tsp_nearest_action(td):
     """Step 0: node 0; afterwards the nearest unvisited node to ``current_node``
-    (Euclidean, f32 ``sqrt(dx*dx+dy*dy)``, ties -> lowest index)."""
+    (Euclidean, f32 ``dx*dx+dy*dy`` and its correctly rounded sqrt, ties -> lowest
+    index)."""
     if bool((td["i"] == 0).all()):
         return torch.zeros(td.batch_size[0], dtype=torch.int64)
     locs = td["locs"]
     cur = gather_by_index(locs, td["current_node"])
     diff = locs - cur[:, None, :]
-    dist = torch.sqrt(diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1])
+    dist = _f32_sqrt(diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1])
     dist = dist.masked_fill(~td["action_mask"], float("inf"))
     return dist.argmin(-1)
 
@@ -299,7 +308,7 @@ def cvrp_nearest_action(td):
     locs = td["locs"]
     cur = gather_by_index(locs, td["current_node"].squeeze(-1))
     diff = locs - cur[:, None, :]
-    dist = torch.sqrt(diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1])
+    dist = _f32_sqrt(diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1])
     feas = td["action_mask"].clone()
     feas[:, 0] = False
     dist = dist.masked_fill(~feas, float("inf"))

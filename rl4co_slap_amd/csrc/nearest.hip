@@ -5,7 +5,7 @@
 // Layout: a G-lane group per instance, 64/G instances per wavefront.  Lane `sl` of
 // the group keeps nodes c = sl + G*k (k < EPL) in VGPRs for the whole episode:
 // coordinates, CVRP demand, and a visited bit per node.  One policy step is EPL
-// distance evaluations per lane, a DPP / permlane-swap argmin over the group and
+// squared distances per lane (one sqrt), a DPP / permlane-swap argmin over the group and
 // three lane broadcasts (x, y, demand of the chosen node); nothing is read from
 // memory after the first load and the only per-step store is the step-major action.
 // The oracle's policy (oracle/envs.py tsp_nearest_action / cvrp_nearest_action):
@@ -24,6 +24,44 @@ __device__ __forceinline__ float pick(const float (&v)[EPL], int slot) {
 #pragma unroll
   for (int k = 0; k < EPL; ++k) r = (k == slot) ? v[k] : r;
   return r;
+}
+
+// Lane-local nearest candidate: argmin over the candidates (bit k of `cand`) of the f32
+// distance sqrt(dx*dx + dy*dy), ties -> lowest node index, exactly as torch.argmin over
+// the oracle's distances.  The scan compares squared distances (the same IEEE products
+// and sum) and takes one correctly rounded sqrt, of the minimum.  A larger squared
+// distance can round to the same sqrt only within a relative 2^-22; a lower-index
+// candidate inside that window is resolved with its own sqrt in a branch that is almost
+// never taken.  Returns (+inf, kNoNode) when there is no candidate.
+template <int G, int EPL>
+__device__ __forceinline__ void lane_nearest(float cx, float cy, const float (&px)[EPL],
+                                             const float (&py)[EPL], uint32_t cand, int sl,
+                                             float& best, int& bi) {
+  float sq[EPL];
+  float smin = __builtin_inff();
+  int kmin = -1;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const float dx = px[k] - cx, dy = py[k] - cy;
+    sq[k] = dx * dx + dy * dy;
+    if (((cand >> k) & 1u) && sq[k] < smin) {
+      smin = sq[k];
+      kmin = k;
+    }
+  }
+  best = kmin >= 0 ? sqrtf(smin) : __builtin_inff();
+  bi = kmin >= 0 ? sl + G * kmin : kNoNode;
+  const float win = smin * (1.0f + 0x1p-20f);
+  bool need = false;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) need |= ((cand >> k) & 1u) && k < kmin && sq[k] <= win;
+  if (need) {  // rare: an earlier node whose distance rounds to the same sqrt
+    int kk = kmin;
+#pragma unroll
+    for (int k = EPL - 1; k >= 0; --k)
+      if (((cand >> k) & 1u) && k < kmin && sq[k] <= win && sqrtf(sq[k]) == best) kk = k;
+    bi = sl + G * kk;
+  }
 }
 
 // TSP: step 0 takes node 0, steps 1..N-1 the nearest unvisited node.
@@ -59,16 +97,9 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
     double len = 0.0;
     int cur = 0;
     for (int t = 1; t < N; ++t) {
-      float best = __builtin_inff();
-      int bi = kNoNode;
-#pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        const float d = edge_len(cx, cy, px[k], py[k]);
-        if (!((vis >> k) & 1u) && d < best) {
-          best = d;
-          bi = sl + G * k;
-        }
-      }
+      float best;
+      int bi;
+      lane_nearest<G, EPL>(cx, cy, px, py, ~vis, sl, best, bi);
       grp_argmin<G>(best, bi);  // t < N: an unvisited node remains
       const int owner = bi % G, slot = bi / G;
       if (sl == owner) vis |= 1u << slot;
@@ -145,18 +176,16 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
     double dist = 0.0;
     for (int t = 0; t < max_steps; ++t) {
       if (__ballot(!done) == 0) break;  // wave-uniform: the group reductions need every lane
-      float best = __builtin_inff();
-      int bi = kNoNode;
+      uint32_t cand = 0;
 #pragma unroll
       for (int k = 0; k < EPL; ++k) {
         const int c = sl + G * k;
         const bool feas = c >= 1 && !((vis >> k) & 1u) && !(dm[k] + used > vcap);
-        const float d = edge_len(cx, cy, px[k], py[k]);
-        if (feas && d < best) {
-          best = d;
-          bi = c;
-        }
+        cand |= (uint32_t)feas << k;
       }
+      float best;
+      int bi;
+      lane_nearest<G, EPL>(cx, cy, px, py, cand, sl, best, bi);
       grp_argmin<G>(best, bi);
       if (done) continue;
       const int a = bi == kNoNode ? 0 : bi;

@@ -193,3 +193,47 @@ def test_cvrp_fused_truncation_flag(dev):
     torch.cuda.synchronize()
     with pytest.raises(RuntimeError, match="not done"):
         ep.final_state()
+
+
+def _sqrt_tie_pair(c):
+    """Two points whose f32 squared distances to `c` differ while their correctly rounded
+    f32 sqrt is equal (found by nudging one coordinate by single ulps)."""
+    g = torch.Generator().manual_seed(0)
+    for _ in range(10000):
+        a = torch.rand(2, generator=g) * 0.5 + 0.25
+        b = a.clone()
+        for _ in range(4):
+            b[0] = torch.nextafter(b[0], torch.tensor(2.0))
+            da, db = a - c, b - c
+            sa = da[0] * da[0] + da[1] * da[1]
+            sb = db[0] * db[0] + db[1] * db[1]
+            ra, rb = torch.sqrt(sa.double()).float(), torch.sqrt(sb.double()).float()
+            if sa != sb and ra == rb:  # correctly rounded sqrt (see oracle/envs.py _f32_sqrt)
+                return (a, b) if sa < sb else (b, a)
+    raise AssertionError("no tie pair found")
+
+
+@pytest.mark.parametrize("n", [8, 40, 100])
+def test_nearest_sqrt_tie_lowest_index(dev, n):
+    """torch.argmin over rounded distances picks the LOWER index of two nodes whose
+    squared distances differ but round to the same sqrt; the kernels scan squared
+    distances and must repair such ties."""
+    from oracle.envs import tsp_nearest_action  # noqa: F401  (policy under test: rollout)
+
+    c = torch.tensor([0.5, 0.5])
+    near, far = _sqrt_tie_pair(c)  # |far| > |near| in squared distance, same sqrt
+    b = 3
+    locs = torch.rand(b, n, 2) * 0.01 + 5.0  # every other node far away
+    locs[:, 0] = c
+    idx_far, idx_near = 1 + (n // 3), 2 + (n // 2)  # the larger squared distance first
+    locs[:, idx_far], locs[:, idx_near] = far, near
+    env = TSPOracle(num_loc=n, seed=1)
+    from oracle.td import TD
+
+    td = env.reset(TD({"locs": locs.clone()}, [b]))
+    r, tdf, a = ref_rollout(env, td, tsp_nearest_action)
+    assert (a[:, 1] == idx_far).all()  # the reference's choice
+    ep = TSPFusedEpisode(locs.to(dev), None, policy="nearest")
+    ep.run_eager()
+    torch.cuda.synchronize()
+    _check(ep.final_state(), a, r, tdf)
