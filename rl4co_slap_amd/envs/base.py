@@ -142,9 +142,23 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
 
     # -- datasets (base.py:236-286) --------------------------------------------
     def dataset(self, batch_size=[], phase="train", filename=None):
+        """``base.py:236-270``: the phase's file(s) if set (a list gives a dict of named
+        datasets), else generated instances; a missing file falls back to generation."""
+        from ..data import TensorDictDataset
+
+        cls = self.dataset_cls if self.dataset_cls is not None else TensorDictDataset
         f = getattr(self, f"{phase}_file") if filename is None else filename
-        td = self.generator(batch_size) if f is None else self.load_data(f, batch_size)
-        return td if self.dataset_cls is None else self.dataset_cls(td)
+        if f is None:
+            td = self.generator(batch_size)
+        else:
+            try:
+                if isinstance(f, Iterable) and not isinstance(f, str):
+                    names = getattr(self, f"{phase}_dataloader_names")
+                    return {name: cls(self.load_data(_f, batch_size)) for name, _f in zip(names, f)}
+                td = self.load_data(f, batch_size)
+            except FileNotFoundError:
+                td = self.generator(batch_size)
+        return cls(td)
 
     @staticmethod
     def load_data(fpath, batch_size=[]):
