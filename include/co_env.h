@@ -177,6 +177,18 @@ int co_decode_step(int64_t batch, int64_t n_actions, const float* logits, int64_
                    float* logprobs_full, uint64_t seed, uint64_t offset, int32_t* status,
                    void* stream);
 
+/* co_decode_step with the top-k / top-p filters of process_logits (decoding.py:112-138,
+ * 183-187) applied after the temperature: top_k > 0 keeps values >= the k-th largest
+ * (torch.topk, multiplicity counted); 0 < top_p < 1 drops elements whose ascending
+ * cumulative softmax probability (ties by index) is <= 1 - top_p.  top_k = 0 / top_p = 0
+ * disable them (co_decode_step == this with 0, 0). */
+int co_decode_step_ex(int64_t batch, int64_t n_actions, const float* logits,
+                      int64_t logits_row_stride, const uint8_t* mask, float tanh_clipping,
+                      float temperature, int top_k, double top_p, int mode,
+                      const int64_t* action_in, int64_t* action_out, float* logp_selected,
+                      float* logp_full, uint64_t seed, uint64_t offset, int32_t* status,
+                      void* stream);
+
 /* co_decode_step fused with TSPEnv._step (tsp/env.py:67-93) for the selected action:
  * mask_out = mask_in minus the action (in-place NOT allowed), i_out = i_in + 1,
  * first_out = first_mode ? action : first_in, done = nothing left, step_reward = 0,

@@ -8,8 +8,24 @@ import torch.nn.functional as F
 from .ops import batchify, gather_by_index
 
 
-def process_logits(logits, mask=None, temperature=1.0, tanh_clipping=0.0, mask_logits=True):
-    """``decoding.py:141-191`` without top-k/top-p (default off)."""
+def top_k_filter(logits, top_k):  # decoding.py:112-117
+    remove = logits < torch.topk(logits, top_k)[0][..., -1, None]
+    return logits.masked_fill(remove, float("-inf"))
+
+
+def top_p_filter(logits, top_p):  # decoding.py:120-138
+    if top_p <= 0.0 or top_p >= 1.0:
+        return logits
+    sorted_logits, sorted_indices = torch.sort(logits, descending=False, stable=True)
+    cumulative_probs = sorted_logits.softmax(dim=-1).cumsum(dim=-1)
+    sorted_remove = cumulative_probs <= (1 - top_p)
+    remove = sorted_remove.scatter(-1, sorted_indices, sorted_remove)
+    return logits.masked_fill(remove, float("-inf"))
+
+
+def process_logits(logits, mask=None, temperature=1.0, tanh_clipping=0.0, mask_logits=True,
+                   top_k=0, top_p=0.0):
+    """``decoding.py:141-191`` (ties of the top-p sort in index order: stable sort)."""
     if tanh_clipping > 0:
         logits = torch.tanh(logits) * tanh_clipping
     if mask_logits:
@@ -17,6 +33,11 @@ def process_logits(logits, mask=None, temperature=1.0, tanh_clipping=0.0, mask_l
         logits = logits.clone()
         logits[~mask] = float("-inf")
     logits = logits / temperature
+    if top_k > 0:
+        logits = top_k_filter(logits, min(top_k, logits.size(-1)))
+    if top_p > 0:
+        assert top_p <= 1.0, "top-p should be in (0, 1]."
+        logits = top_p_filter(logits, top_p)
     return F.log_softmax(logits, dim=-1)
 
 

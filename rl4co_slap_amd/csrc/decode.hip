@@ -107,15 +107,89 @@ struct DecodeRow {
   __device__ __forceinline__ void run(bool valid, int N, const float* lrow, const uint8_t* mrow,
                                       float clip, float temp, int mode, int64_t a_in,
                                       uint64_t seed, uint64_t offset, int64_t row, int sl,
-                                      int grp) {
+                                      int grp, int top_k = 0, double top_p = 0.0) {
     load(valid, N, lrow, mrow, sl);
-    compute(valid, N, clip, temp, mode, a_in, seed, offset, row, sl, grp);
+    compute(valid, N, clip, temp, mode, a_in, seed, offset, row, sl, grp, top_k, top_p);
+  }
+
+  // decoding.py:112-117 modify_logits_for_top_k_filtering on x (the processed logits):
+  // threshold = the k-th largest value counted with multiplicity (torch.topk), values
+  // strictly below it -> -inf.  Distinct levels are peeled from the top with a group max
+  // and a group count; a row with fewer than k finite values keeps everything.
+  __device__ __forceinline__ void filter_top_k(int N, int top_k, int sl) {
+    const float NEG_INF = -__builtin_inff();
+    const int c0 = sl * EPL;
+    float hi = __builtin_inff(), thr = NEG_INF;
+    int remaining = top_k;
+    for (int it = 0; it < top_k; ++it) {
+      float lm = NEG_INF;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k)
+        if (c0 + k < N && x[k] < hi) lm = fmaxf(lm, x[k]);
+      lm = grp_max<RL>(lm);
+      if (lm == NEG_INF) break;
+      int cnt = 0;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) cnt += (c0 + k < N) && (x[k] == lm);
+      cnt = (int)grp_reduce<RL>((uint32_t)cnt, [](uint32_t a, uint32_t b) { return a + b; });
+      if (cnt >= remaining) {
+        thr = lm;
+        break;
+      }
+      remaining -= cnt;
+      hi = lm;
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) x[k] = x[k] < thr ? NEG_INF : x[k];
+  }
+
+  // decoding.py:120-138 modify_logits_for_top_p_filtering: with p = softmax(x) and the
+  // ascending order (ties by index), drop every element whose cumulative probability up
+  // to and including itself is <= 1 - top_p.  Each lane accumulates, for its elements,
+  // the probabilities of the row's elements that precede them (group broadcasts of the
+  // row); the summation order differs from ATen's sorted cumsum, so an element whose
+  // cumulative sum lies within rounding of the threshold can be decided differently.
+  __device__ __forceinline__ void filter_top_p(bool valid, int N, double top_p, float m, int sl,
+                                               int grp) {
+    const float NEG_INF = -__builtin_inff();
+    const int c0 = sl * EPL;
+    float pr[EPL], s = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      pr[k] = (valid && c0 + k < N) ? expf(x[k] - m) : 0.f;
+      s += pr[k];
+    }
+    s = grp_sum<RL>(s);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) pr[k] = pr[k] / s;
+    float cum[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) cum[k] = 0.f;
+    for (int j = 0; j < N; ++j) {
+      const int owner = grp * RL + j / EPL, slot = j % EPL;
+      float xs = 0.f, ps = 0.f;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        xs = k == slot ? x[k] : xs;
+        ps = k == slot ? pr[k] : ps;
+      }
+      const float vj = __shfl(xs, owner, 64), pj = __shfl(ps, owner, 64);
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        const bool before = vj < x[k] || (vj == x[k] && j <= c0 + k);
+        cum[k] += before ? pj : 0.f;
+      }
+    }
+    const float keep_above = (float)(1.0 - top_p);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) x[k] = cum[k] <= keep_above ? NEG_INF : x[k];
   }
 
   // the math on data already `load`ed (callers overlap several rows' loads)
   __device__ __forceinline__ void compute(bool valid, int N, float clip, float temp, int mode,
                                           int64_t a_in, uint64_t seed, uint64_t offset,
-                                          int64_t row, int sl, int grp) {
+                                          int64_t row, int sl, int grp, int top_k = 0,
+                                          double top_p = 0.0) {
     const float NEG_INF = -__builtin_inff();
     const int c0 = sl * EPL;
     float m = NEG_INF;
@@ -132,6 +206,8 @@ struct DecodeRow {
       x[k] = v;
     }
     m = grp_max<RL>(m);
+    if (top_k > 0 && top_k < N) filter_top_k(N, top_k, sl);
+    if (top_p > 0.0 && top_p < 1.0) filter_top_p(valid, N, top_p, m, sl, grp);
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < EPL; ++k)
@@ -206,7 +282,8 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
                                                      float clip, float temp, int mode,
                                                      const int64_t* action_in, int64_t* action_out,
                                                      float* logp_sel, float* full, uint64_t seed,
-                                                     uint64_t offset, int32_t* status) {
+                                                     uint64_t offset, int32_t* status, int top_k,
+                                                     double top_p) {
   constexpr int RPW = 64 / RL;
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -218,7 +295,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
     const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
     DecodeRow<RL, EPL, VEC> d;
     d.run(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, clip, temp,
-          mode, a_in, seed, offset, row, sl, grp);
+          mode, a_in, seed, offset, row, sl, grp, top_k, top_p);
     if (!valid) continue;
     if (full) {
 #pragma unroll
@@ -341,12 +418,13 @@ inline bool decode_vec_ok(const float* logits, int64_t lstride, const uint8_t* m
 
 }  // namespace
 
-extern "C" int co_decode_step(int64_t B, int64_t N, const float* logits, int64_t lstride,
-                              const uint8_t* mask, float clip, float temp, int mode,
-                              const int64_t* action_in, int64_t* action_out, float* logp_sel,
-                              float* full, uint64_t seed, uint64_t offset, int32_t* status,
-                              void* stream) {
-  if (B < 0 || N <= 0 || N > 64 * 32) return CO_E_INVAL;
+extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int64_t lstride,
+                                 const uint8_t* mask, float clip, float temp, int top_k,
+                                 double top_p, int mode, const int64_t* action_in,
+                                 int64_t* action_out, float* logp_sel, float* full, uint64_t seed,
+                                 uint64_t offset, int32_t* status, void* stream) {
+  if (B < 0 || N <= 0 || N > 64 * 32 || top_k < 0 || top_p < 0.0 || top_p > 1.0)
+    return CO_E_INVAL;
   if (mode < 0 || mode > 2) return CO_E_MODE;
   if (B == 0) return CO_OK;
   if (!logits || !action_out) return CO_E_INVAL;
@@ -356,7 +434,7 @@ extern "C" int co_decode_step(int64_t B, int64_t N, const float* logits, int64_t
 #define CO_DECODE(RL, EPL, V)                                                                  \
   hipLaunchKernelGGL((decode_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N, logits,        \
                      lstride, mask, clip, temp, mode, action_in, action_out, logp_sel, full,   \
-                     seed, offset, status)
+                     seed, offset, status, top_k, top_p)
   if (decode_vec_ok(logits, lstride, mask, N)) {
     CO_ROW_DISPATCH(CO_DECODE, true);
   } else {
@@ -364,6 +442,15 @@ extern "C" int co_decode_step(int64_t B, int64_t N, const float* logits, int64_t
   }
 #undef CO_DECODE
   return launch_status();
+}
+
+extern "C" int co_decode_step(int64_t B, int64_t N, const float* logits, int64_t lstride,
+                              const uint8_t* mask, float clip, float temp, int mode,
+                              const int64_t* action_in, int64_t* action_out, float* logp_sel,
+                              float* full, uint64_t seed, uint64_t offset, int32_t* status,
+                              void* stream) {
+  return co_decode_step_ex(B, N, logits, lstride, mask, clip, temp, 0, 0.0, mode, action_in,
+                           action_out, logp_sel, full, seed, offset, status, stream);
 }
 
 extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int64_t lstride,

@@ -5,8 +5,8 @@ tanh clipping, masking, temperature, ``log_softmax``, greedy argmax / Philox
 sampling / evaluate, and the logprob gather.  The greedy/sampling feasibility
 assertion (``decoding.py:376-379,393-395``) is recorded in a device status word
 and raised once in ``post_decoder_hook`` instead of synchronising every step.
-Top-k / top-p filtering, beam search and multi-sampling are out of scope
-(SURVEY.md section 8f).
+Top-k / top-p filtering runs inside the same launch (``co_decode_step_ex``); beam
+search and multi-sampling are out of scope.
 """
 from __future__ import annotations
 
@@ -23,7 +23,8 @@ _MODES = {"greedy": 0, "sampling": 1, "evaluate": 2}
 
 
 def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, action=None,
-                return_full=False, seed=None, offset=0, status=None):
+                return_full=False, seed=None, offset=0, status=None, top_k: int = 0,
+                top_p: float = 0.0):
     """One fused decode step.  Returns ``(action[B], logp[B], full_logprobs or None)``."""
     nat.require_device(logits, mask, action)
     if logits.dtype != torch.float32:
@@ -41,22 +42,27 @@ def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, act
         action = action.long().contiguous()
     if seed is None:
         seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
-    nat.call("co_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
-             float(tanh_clipping), float(temperature), _MODES[mode], nat.ptr(action),
-             nat.ptr(act_out), nat.ptr(logp), nat.ptr(full), seed, offset, nat.ptr(status),
-             nat.stream_of(logits))
+    if top_k > 0 or top_p > 0:
+        assert top_p <= 1.0, "top-p should be in (0, 1]."
+        nat.call("co_decode_step_ex", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
+                 float(tanh_clipping), float(temperature), min(int(top_k), n), float(top_p),
+                 _MODES[mode], nat.ptr(action), nat.ptr(act_out), nat.ptr(logp), nat.ptr(full),
+                 seed, offset, nat.ptr(status), nat.stream_of(logits))
+    else:
+        nat.call("co_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
+                 float(tanh_clipping), float(temperature), _MODES[mode], nat.ptr(action),
+                 nat.ptr(act_out), nat.ptr(logp), nat.ptr(full), seed, offset, nat.ptr(status),
+                 nat.stream_of(logits))
     return act_out, logp, full
 
 
 def process_logits(logits, mask=None, temperature: float = 1.0, top_p: float = 0.0,
                    top_k: int = 0, tanh_clipping: float = 0, mask_logits: bool = True):
-    """``decoding.py:141-191`` -> full log-probabilities (top-k/top-p unsupported)."""
-    if top_k > 0 or top_p > 0:
-        raise NotImplementedError("top-k / top-p filtering is not on the MI355X hot path")
+    """``decoding.py:141-191`` -> full log-probabilities."""
     if mask_logits:
         assert mask is not None, "mask must be provided if mask_logits is True"
     _, _, full = decode_step(logits, mask if mask_logits else None, "greedy", temperature,
-                             tanh_clipping, return_full=True)
+                             tanh_clipping, return_full=True, top_k=top_k, top_p=top_p)
     return full
 
 
@@ -103,8 +109,6 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
                  select_start_nodes_fn: Optional[callable] = None,
                  improvement_method_mode: bool = False, select_best: bool = False,
                  store_all_logp: bool = False, key: str = "action", **kwargs):
-        if top_k > 0 or top_p > 0:
-            raise NotImplementedError("top-k / top-p filtering is not on the MI355X hot path")
         self.temperature, self.top_p, self.top_k = temperature, top_p, top_k
         self.mask_logits, self.tanh_clipping = mask_logits, tanh_clipping
         self.multistart, self.multisample = multistart, multisample
@@ -162,7 +166,8 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         act_in = action if mode == "evaluate" else None
         sel, logp, full = decode_step(logits, mask, mode, self.temperature, self.tanh_clipping,
                                       action=act_in, return_full=self.store_all_logp,
-                                      offset=self._step_idx, status=self._status)
+                                      offset=self._step_idx, status=self._status,
+                                      top_k=self.top_k, top_p=self.top_p)
         self._step_idx += 1
         if mode == "evaluate":
             sel = action

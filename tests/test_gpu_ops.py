@@ -159,3 +159,50 @@ def test_tsp_reward_stepmajor_shared_locs(dev, lb, s, n):
              nat.ptr(st), nat.stream_of(out))
     torch.cuda.synchronize()
     assert int(st.item()) & nat.ST_INVALID_TOUR
+
+
+def _top_p_margin(logits, mask, top_p):
+    """Distance of every row's ascending cumulative probabilities from 1 - top_p (the
+    oracle's), to skip rows whose decision is within float rounding."""
+    x = logits.masked_fill(~mask, float("-inf"))
+    srt = torch.sort(x, descending=False, stable=True)[0]
+    cum = srt.softmax(-1).cumsum(-1)
+    return (cum - (1 - top_p)).abs().min(-1).values
+
+
+@pytest.mark.parametrize("n", [20, 100, 129])
+@pytest.mark.parametrize("top_k,top_p", [(5, 0.0), (1, 0.0), (0, 0.9), (0, 0.5), (10, 0.7)])
+def test_decode_top_k_top_p(dev, n, top_k, top_p):
+    from rl4co_slap_amd.utils.decoding import process_logits
+
+    g = torch.Generator().manual_seed(n + top_k)
+    b = 256
+    logits = torch.randn(b, n, generator=g) * 2
+    mask = _rand_mask(b, n, g)
+    want = odec.process_logits(logits, mask, top_k=top_k, top_p=top_p)
+    got = process_logits(logits.to(dev), mask.to(dev), top_k=top_k, top_p=top_p).cpu()
+    rows = torch.ones(b, dtype=torch.bool)
+    if top_p > 0:
+        rows = _top_p_margin(logits, mask, top_p) > 1e-5
+        assert rows.float().mean() > 0.9
+    assert torch.equal(got[rows].isinf(), want[rows].isinf())
+    fin = rows[:, None] & want.isfinite()
+    assert torch.allclose(got[fin], want[fin], rtol=1e-5, atol=1e-5)
+
+
+def test_decode_top_k_duplicates_and_sampling(dev):
+    from rl4co_slap_amd.utils.decoding import decode_step, process_logits
+
+    g = torch.Generator().manual_seed(11)
+    b, n = 128, 50
+    logits = (torch.randn(b, n, generator=g) * 2).round()  # many exact duplicates
+    mask = torch.ones(b, n, dtype=torch.bool)
+    for k in (1, 3, 7, 50):
+        want = odec.process_logits(logits, mask, top_k=k)
+        got = process_logits(logits.to(dev), mask.to(dev), top_k=k).cpu()
+        assert torch.equal(got.isinf(), want.isinf()), k
+    keep = odec.process_logits(logits, mask, top_k=4).isfinite()
+    for off in range(8):
+        a, _, _ = decode_step(logits.to(dev), mask.to(dev), "sampling", top_k=4, seed=5,
+                              offset=off)
+        assert keep.gather(1, a.cpu()[:, None]).all()
