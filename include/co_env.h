@@ -301,6 +301,18 @@ int co_dihedral8_augment(int64_t batch, int64_t num_loc, const float* xy, float*
 int co_symmetric_augment(int64_t batch, int64_t num_loc, const float* xy, const float* phi,
                          float offset, float* out, void* stream);
 
+/* BeamSearch._make_beam_step (rl4co/utils/decoding.py:611-641): rows e = s*B + b of
+ * logp[BW*B, N] (full log-probabilities of the beams) plus parent[e] are ranked per
+ * instance over the BW*N (beam, node) candidates; the BW best (descending; equal scores
+ * -> lower candidate index s*N + c) are written to rows j*B + b: selected node,
+ * beam_parent s, beam_row = b + s*B (the state row to continue from) and the new parent
+ * score.  mask != NULL: a selected node with mask 0 sets CO_ST_INFEASIBLE
+ * (decoding.py:519-522).  BW*N <= 36864. */
+int co_beam_select(int64_t batch, int64_t beam_width, int64_t n_actions, const float* logp,
+                   int64_t logp_row_stride, const float* parent, const uint8_t* mask,
+                   int64_t* selected, int32_t* beam_parent, int64_t* beam_row,
+                   float* score_out, int32_t* status, void* stream);
+
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 

@@ -119,4 +119,84 @@ class Decoding:
         return torch.stack(self.logprobs, 1), torch.stack(self.actions, 1), td, env
 
 
-__all__ = ["process_logits", "greedy", "sampling", "get_log_likelihood", "Decoding", "batchify"]
+class BeamSearchOracle:
+    """``decoding.py:500-641`` (``BeamSearch``) restated with plain torch ops on the
+    oracle's TD: start nodes, then per step the top ``beam_width`` of the (beam, node)
+    candidates per instance, state rows re-indexed by the beam parents, backtracking
+    and best-beam selection by reward."""
+
+    def __init__(self, beam_width=None, select_best=True, temperature=1.0, tanh_clipping=0.0,
+                 mask_logits=True, **unused):
+        self.beam_width, self.select_best = beam_width, select_best
+        self.temperature, self.tanh_clipping, self.mask_logits = temperature, tanh_clipping, mask_logits
+        self.actions, self.logprobs, self.beam_path = [], [], []
+        self.parent_beam_logprobs = None
+
+    @staticmethod
+    def _rows(td, idx):
+        from .td import TD
+        return TD({k: v[idx] for k, v in td.items()}, [idx.shape[0]])
+
+    def pre_decoder_hook(self, td, env):  # decoding.py:526-556
+        from .td import batchify_td
+        if self.beam_width is None:
+            self.beam_width = env.get_num_starts(td)
+        action = env.select_start_nodes(td, num_starts=self.beam_width)
+        td = batchify_td(td, self.beam_width)
+        td["action"] = action
+        td = env.step(td)["next"]
+        logprobs = torch.zeros(td["action_mask"].shape)
+        self.logprobs.append(logprobs)
+        self.actions.append(action)
+        self.parent_beam_logprobs = logprobs.gather(1, action[..., None])
+        self.beam_path.append(torch.zeros(logprobs.size(0), dtype=torch.int32))
+        return td, env, self.beam_width
+
+    def step(self, logits, mask, td, action=None):  # decoding.py:327-369, 512-524, 611-641
+        m = mask if self.mask_logits else None
+        logp = process_logits(logits, m, self.temperature, self.tanh_clipping, self.mask_logits)
+        e, n = logp.shape
+        b = e // self.beam_width
+        seq = torch.arange(0, b).repeat(self.beam_width)
+        hst = torch.cat((logp + self.parent_beam_logprobs).split(b), dim=1)
+        topv, topi = torch.topk(hst, self.beam_width, dim=1)
+        sel_lp = torch.hstack(torch.unbind(topv, 1)).unsqueeze(1)
+        topi = torch.hstack(torch.unbind(topi, 1))
+        selected = topi % n
+        parent = (topi // n).int()
+        idx = seq + parent * b
+        self.parent_beam_logprobs = sel_lp
+        self.beam_path.append(parent)
+        td = self._rows(td, idx)
+        logp = logp[idx]
+        if m is not None:
+            assert not (~m[idx]).gather(1, selected.unsqueeze(-1)).any(), "infeasible action selected"
+        td["action"] = selected
+        self.actions.append(selected)
+        self.logprobs.append(logp)
+        return td
+
+    def post_decoder_hook(self, td, env):  # decoding.py:558-609
+        actions = torch.stack(self.actions, 1)
+        logprobs = torch.stack(self.logprobs, 1)
+        cur = self.beam_path[-1]
+        seqs, lps = [actions[:, -1]], [logprobs[:, -1]]
+        b = actions.size(0) // self.beam_width
+        seq = torch.arange(0, b).repeat(self.beam_width)
+        for k in reversed(range(len(self.beam_path) - 1)):
+            idx = seq + cur * b
+            seqs.append(actions[idx, k])
+            lps.append(logprobs[idx, k])
+            cur = self.beam_path[k][idx]
+        actions = torch.stack(list(reversed(seqs)), dim=1)
+        logprobs = torch.stack(list(reversed(lps)), dim=1)
+        if not self.select_best:
+            return logprobs, actions, td, env
+        rewards = env.get_reward(td, actions)
+        _, idx = torch.cat(rewards.unsqueeze(1).split(b), 1).max(1)
+        flat = torch.arange(b) + idx * b
+        return logprobs[flat], actions[flat], self._rows(td, flat), env
+
+
+__all__ = ["process_logits", "greedy", "sampling", "get_log_likelihood", "Decoding",
+           "BeamSearchOracle", "batchify"]

@@ -30,7 +30,11 @@ def constructive_forward(td, env, logits_fn, decode_type="greedy", actions=None,
     consumer of the env API and out of scope)."""
     if actions is not None:
         decode_type = "evaluate"
-    strat = Decoding(decode_type, **decoding_kwargs)
+    if decode_type == "beam_search":
+        from .decoding import BeamSearchOracle
+        strat = BeamSearchOracle(**decoding_kwargs)
+    else:
+        strat = Decoding(decode_type, **decoding_kwargs)
     td, env, num_starts = strat.pre_decoder_hook(td, env)
     step = 0
     while not td["done"].all():

@@ -484,3 +484,82 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
 #undef CO_TDS
   return launch_status();
 }
+
+// --------------------------------------------------------------------- beam search
+// BeamSearch._make_beam_step (decoding.py:611-641) + the feasibility assert of _step
+// (:512-524): for instance b, candidate t = s*N + c (beam s, node c) scores
+// logp[s*B + b, c] + parent[s*B + b] (f32 add, as the reference's broadcast add); the
+// BW best (torch.topk, sorted; equal scores -> lower t) go to rows j*B + b:
+// selected = t % N, beam_parent = t / N, beam row = b + beam_parent*B, new parent score.
+// One wave per instance: the BW*N scores are staged in LDS, then BW rounds of a wave
+// argmax over the untaken ones (a taken bitmap in LDS).
+namespace {
+__global__ __launch_bounds__(64) void beam_select_kernel(
+    int64_t B, int BW, int N, const float* __restrict__ logp, int64_t lstride,
+    const float* __restrict__ parent, const uint8_t* __restrict__ mask,
+    int64_t* __restrict__ selected, int32_t* __restrict__ beam_parent,
+    int64_t* __restrict__ beam_row, float* __restrict__ score_out, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int T = BW * N;
+  float* sc = reinterpret_cast<float*>(smem);
+  uint32_t* taken = reinterpret_cast<uint32_t*>(sc + T);
+  const int lane = threadIdx.x;
+  for (int64_t b = blockIdx.x; b < B; b += gridDim.x) {
+    for (int t = lane; t < T; t += 64) {
+      const int s = t / N, c = t - s * N;
+      const int64_t r = (int64_t)s * B + b;
+      sc[t] = logp[r * lstride + c] + parent[r];
+    }
+    for (int w = lane; w < (T + 31) / 32; w += 64) taken[w] = 0u;
+    __syncthreads();
+    bool bad = false;
+    for (int j = 0; j < BW; ++j) {
+      float bv = -__builtin_inff();
+      int bi = 0x7fffffff;
+      for (int t = lane; t < T; t += 64) {
+        const bool free_t = !((taken[t >> 5] >> (t & 31)) & 1u);
+        const float v = sc[t];
+        if (free_t && (v > bv || (v == bv && t < bi) || bi == 0x7fffffff)) {
+          bv = v;
+          bi = t;
+        }
+      }
+      wave_argmax(bv, bi);  // ties -> lower index
+      if (bi == 0x7fffffff) bi = 0;
+      const int s = bi / N, c = bi - s * N;
+      if (lane == 0) {
+        taken[bi >> 5] |= 1u << (bi & 31);
+        const int64_t row = (int64_t)j * B + b;
+        selected[row] = c;
+        beam_parent[row] = s;
+        beam_row[row] = b + (int64_t)s * B;
+        score_out[row] = bv;
+        if (mask && !mask[(b + (int64_t)s * B) * N + c]) bad = true;
+      }
+      __syncthreads();
+    }
+    if (bad) set_status(status, CO_ST_INFEASIBLE);
+    __syncthreads();
+  }
+}
+}  // namespace
+
+extern "C" int co_beam_select(int64_t B, int64_t BW, int64_t N, const float* logp,
+                              int64_t lstride, const float* parent, const uint8_t* mask,
+                              int64_t* selected, int32_t* beam_parent, int64_t* beam_row,
+                              float* score_out, int32_t* status, void* stream) {
+  if (B < 0 || BW <= 0 || N <= 0 || BW > N * BW || BW * N > 36 * 1024) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!logp || !parent || !selected || !beam_parent || !beam_row || !score_out ||
+      (mask && !status))
+    return CO_E_INVAL;
+  const int T = (int)(BW * N);
+  const size_t shmem = (size_t)T * 4 + (size_t)((T + 31) / 32) * 4;
+  if (shmem > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)beam_select_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
+  hipLaunchKernelGGL(beam_select_kernel, dim3((unsigned)(B < 65536 ? B : 65536)), dim3(64),
+                     shmem, (hipStream_t)stream, B, (int)BW, (int)N, logp, lstride, parent,
+                     mask, selected, beam_parent, beam_row, score_out, status);
+  return launch_status();
+}

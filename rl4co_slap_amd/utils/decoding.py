@@ -5,8 +5,9 @@ tanh clipping, masking, temperature, ``log_softmax``, greedy argmax / Philox
 sampling / evaluate, and the logprob gather.  The greedy/sampling feasibility
 assertion (``decoding.py:376-379,393-395``) is recorded in a device status word
 and raised once in ``post_decoder_hook`` instead of synchronising every step.
-Top-k / top-p filtering runs inside the same launch (``co_decode_step_ex``); beam
-search and multi-sampling are out of scope.
+Top-k / top-p filtering runs inside the same launch (``co_decode_step_ex``); beam search
+ranks the beams' candidates with ``co_beam_select`` and re-indexes the state rows with
+the device gather.  Multi-sampling is out of scope.
 """
 from __future__ import annotations
 
@@ -216,10 +217,131 @@ class Evaluate(DecodingStrategy):
         return "evaluate"
 
 
+def _take_rows(td, idx):
+    """``td[idx]`` for a TensorDict whose columns all lead with the batch dim: one device
+    gather per column."""
+    out = {}
+    for k, v in td.items():
+        if not torch.is_tensor(v) or v.dim() == 0:
+            out[k] = v
+        elif v.dim() == 1:
+            out[k] = gather_by_index(v[:, None], idx, dim=0).squeeze(-1)
+        else:
+            out[k] = gather_by_index(v, idx, dim=0, squeeze=False)
+    return TensorDict(out, batch_size=[idx.shape[0]])
+
+
+class BeamSearch(DecodingStrategy):
+    """``decoding.py:500-641``: beam width defaults to the env's number of starts; the
+    first step takes the start nodes, then every step ranks the BW x N (beam, node)
+    candidates per instance on the device (``co_beam_select``)."""
+
+    name = "beam_search"
+
+    def __init__(self, beam_width=None, select_best=True, **kwargs):
+        kwargs["store_all_logp"] = True
+        super().__init__(**kwargs)
+        self.beam_width = beam_width
+        self.select_best = select_best
+        self.parent_beam_logprobs = None
+        self.beam_path = []
+
+    def _mode(self):
+        return "greedy"
+
+    def pre_decoder_hook(self, td, env, action=None):
+        """``decoding.py:526-556``."""
+        if self.beam_width is None:
+            self.beam_width = env.get_num_starts(td)
+        assert self.beam_width > 1, "beam width must be larger than 1"
+        if self.select_start_nodes_fn is not None:
+            action = self.select_start_nodes_fn(td, env, self.beam_width)
+        else:
+            action = env.select_start_nodes(td, num_starts=self.beam_width)
+        td = batchify(td, self.beam_width)
+        td.set("action", action)
+        td = env.step(td)["next"]
+        logprobs = torch.zeros(td["action_mask"].shape, dtype=torch.float32, device=td.device)
+        self.logprobs.append(logprobs)
+        self.actions.append(action)
+        self.parent_beam_logprobs = torch.zeros((action.shape[0], 1), dtype=torch.float32,
+                                                device=td.device)
+        self.beam_path.append(torch.zeros(action.shape[0], dtype=torch.int32, device=td.device))
+        self.num_starts = self.beam_width
+        return td, env, self.beam_width
+
+    def step(self, logits, mask, td: TensorDict = None, action=None, env=None, **kwargs):
+        """``decoding.py:327-369`` with ``_step`` = ``decoding.py:512-524`` + ``:611-641``."""
+        if not self.mask_logits:
+            mask = None
+        if self._status is None:
+            self._status = nat.scratch_status(logits.device)
+        _, _, full = decode_step(logits, mask, "greedy", self.temperature, self.tanh_clipping,
+                                 return_full=True, top_k=self.top_k, top_p=self.top_p)
+        e, n = full.shape
+        b = e // self.beam_width
+        dev = full.device
+        sel = torch.empty(e, dtype=torch.int64, device=dev)
+        parent = torch.empty(e, dtype=torch.int32, device=dev)
+        rows = torch.empty(e, dtype=torch.int64, device=dev)
+        score = torch.empty(e, dtype=torch.float32, device=dev)
+        par = self.parent_beam_logprobs.reshape(e).contiguous()
+        m = mask.contiguous() if mask is not None else None
+        nat.call("co_beam_select", b, self.beam_width, n, nat.ptr(full), full.stride(0),
+                 nat.ptr(par), nat.ptr(m), nat.ptr(sel), nat.ptr(parent), nat.ptr(rows),
+                 nat.ptr(score), nat.ptr(self._status), nat.stream_of(full))
+        self.parent_beam_logprobs = score[:, None]
+        self.beam_path.append(parent)
+        td = _take_rows(td, rows)
+        logprobs = gather_by_index(full, rows, dim=0, squeeze=False)
+        td.set(self.key, sel)
+        self.actions.append(sel)
+        self.logprobs.append(logprobs)
+        return td
+
+    def post_decoder_hook(self, td, env):
+        """``decoding.py:558-565``."""
+        if self._status is not None and int(self._status.item()) & nat.ST_INFEASIBLE:
+            raise AssertionError("infeasible action selected")
+        actions, logprobs = self._backtrack()
+        if self.select_best:
+            return self._select_best_beam(logprobs, actions, td, env)
+        return logprobs, actions, td, env
+
+    def _backtrack(self):
+        """``decoding.py:567-599``: follow the parents back from the last step."""
+        actions = torch.stack(self.actions, 1)
+        logprobs = torch.stack(self.logprobs, 1)
+        assert actions.size(1) == len(self.beam_path), "action idx shape and beam path shape dont match"
+        cur_parent = self.beam_path[-1].long()
+        seqs, lps = [actions[:, -1]], [logprobs[:, -1]]
+        e = actions.size(0)
+        b = e // self.beam_width
+        seq = torch.arange(0, b, device=actions.device).repeat(self.beam_width)
+        for k in reversed(range(len(self.beam_path) - 1)):
+            idx = seq + cur_parent * b
+            seqs.append(gather_by_index(actions[:, k].contiguous()[:, None], idx, dim=0).squeeze(-1))
+            lps.append(gather_by_index(logprobs[:, k].contiguous(), idx, dim=0, squeeze=False))
+            cur_parent = gather_by_index(self.beam_path[k].long()[:, None], idx, dim=0).squeeze(-1)
+        return (torch.stack(list(reversed(seqs)), dim=1),
+                torch.stack(list(reversed(lps)), dim=1))
+
+    def _select_best_beam(self, logprobs, actions, td, env):
+        """``decoding.py:601-609``."""
+        e = logprobs.size(0)
+        b = e // self.beam_width
+        rewards = env.get_reward(td, actions)
+        _, idx = torch.cat(rewards.unsqueeze(1).split(b), 1).max(1)
+        flat_idx = torch.arange(b, device=rewards.device) + idx * b
+        return (gather_by_index(logprobs, flat_idx, dim=0, squeeze=False),
+                gather_by_index(actions, flat_idx, dim=0, squeeze=False),
+                _take_rows(td, flat_idx), env)
+
+
 def get_decoding_strategy(decoding_strategy, **config):
-    """``decoding.py:17-36`` (beam search / multisampling are out of scope)."""
+    """``decoding.py:17-36`` (multisampling is out of scope)."""
     registry = {"greedy": Greedy, "sampling": Sampling, "multistart_greedy": Greedy,
-                "multistart_sampling": Sampling, "evaluate": Evaluate}
+                "multistart_sampling": Sampling, "evaluate": Evaluate, "beam_search": BeamSearch}
     if "multistart" in decoding_strategy:
         config["multistart"] = True
     return registry.get(decoding_strategy, Sampling)(**config)

@@ -70,3 +70,19 @@ def test_policy_evaluate_and_sampling_consistency(dev):
     _, _, env3, td3 = _pair("tsp", b, n, 9, dev)
     ev = pol(td3, env3, actions=a)
     assert torch.allclose(ev["log_likelihood"], smp["log_likelihood"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("name,b,n,bw", [("tsp", 8, 10, 4), ("tsp", 5, 20, 20), ("cvrp", 6, 12, 3)])
+@pytest.mark.parametrize("select_best", [True, False])
+def test_policy_beam_search_matches_oracle(dev, name, b, n, bw, select_best):
+    ref_env, td_ref, env, td = _pair(name, b, n, 300 + n, dev)
+    ref = constructive_forward(td_ref, ref_env, neg_dist_logits, decode_type="beam_search",
+                               beam_width=bw, select_best=select_best)
+    pol = ConstructivePolicy(None, LogitsDecoder(neg_dist_logits), env_name=name)
+    out = pol(td, env, phase="test", decode_type="beam_search", beam_width=bw,
+              select_best=select_best, return_actions=True)
+    assert torch.equal(out["actions"].cpu(), ref["actions"])
+    r, rr = out["reward"].cpu(), ref["reward"]
+    assert ((r - rr).abs() <= 1e-5 * rr.abs().clamp(min=1)).all()
+    ll, lr = out["log_likelihood"].cpu(), ref["log_likelihood"]
+    assert ((ll - lr).abs() <= 1e-4 * lr.abs().clamp(min=1)).all()
