@@ -170,6 +170,22 @@ __device__ __forceinline__ void grp_argmin(float& v, int& idx) {
   idx = (int)ui;
 }
 
+// Exact group argmin for NaN-free values in two cheap passes: a float group min (one DPP
+// move + v_min per stage), then the group min of the indices of the lanes that hold it
+// (ties -> lowest index, as torch.argmin).  About half the VALU of a (value, index)
+// pair reduction.  A lane without a candidate passes (+inf, 0x7fffffff).
+template <int RL>
+__device__ __forceinline__ void grp_argmin_split(float& v, int& idx) {
+  const float m = __uint_as_float(grp_reduce<RL>(__float_as_uint(v), [](uint32_t a, uint32_t b) {
+    return __float_as_uint(fminf(__uint_as_float(a), __uint_as_float(b)));
+  }));
+  const int cand = v == m ? idx : 0x7fffffff;
+  idx = (int)grp_reduce<RL>((uint32_t)cand, [](uint32_t a, uint32_t b) {
+    return (uint32_t)min((int)a, (int)b);
+  });
+  v = m;
+}
+
 // Zero a device int32 (flags / counters).  A kernel, not hipMemsetAsync: memset nodes
 // captured into HIP graphs were observed on MI355X to replay with a wrong fill byte
 // (0x10101010 after a 4-byte memset to 0), which corrupted counters in replays.

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
       float best;
       int bi;
       lane_nearest<G, EPL>(cx, cy, px, py, ~vis, sl, best, bi);
-      grp_argmin<G>(best, bi);  // t < N: an unvisited node remains
+      grp_argmin_split<G>(best, bi);  // t < N: an unvisited node remains
       const int owner = bi % G, slot = bi / G;
       if (sl == owner) vis |= 1u << slot;
       cx = __shfl(pick(px, slot), gbase + owner, 64);
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
       float best;
       int bi;
       lane_nearest<G, EPL>(cx, cy, px, py, cand, sl, best, bi);
-      grp_argmin<G>(best, bi);
+      grp_argmin_split<G>(best, bi);
       if (done) continue;
       const int a = bi == kNoNode ? 0 : bi;
       const int owner = a % G, slot = a / G;

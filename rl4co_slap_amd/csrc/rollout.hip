@@ -317,24 +317,28 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
   float* olen = s_len + g * O;
   int32_t* pks = s_pk + g * O * K;
 
-  // staged up front so these loads overlap the step loop: coordinates, the initial
-  // assignment and the picklist (as wrapped product indices, -1 = out of range)
-  const float2* lrow = locs + bb * L;
-  for (int c = sl; c < L; c += G) xy[c] = lrow[c];
-  const int64_t* prow = picklist + bb * (int64_t)O * K;
-  for (int c = sl; c < O * K; c += G) {
-    int64_t pp = prow[c];
-    if (pp < 0) pp += P;
-    pks[c] = (pp < 0 || pp >= P) ? -1 : (int32_t)pp;
-  }
-  for (int c = sl; c < P; c += G) asg[c] = assign_in[bb * P + c];
+  // Loads are issued in the order they are needed: the depot distances (the step loop),
+  // then the coordinates and up to G*EPL picklist entries, which stay in registers during
+  // the step loop and go to LDS after it, so their latency hides behind the loop.  The
+  // initial assignment is not read: the P steps overwrite every entry (product t <- step t).
   float dd[EPL];
-  uint32_t avail = 0;  // bit k: location sl + G*k is free
+  uint32_t avail = 0;  // bit k: location sl + G*k is free (the mask output)
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
     const int c = sl + G * k;
-    dd[k] = (CLOSEST && c < L) ? depot_dist[bb * L + c] : 0.f;
-    if (c < L && c != 0) avail |= 1u << k;  // the depot is never free (slap/env.py:115-116)
+    const bool ok = c < L && c != 0;  // the depot is never free (slap/env.py:115-116)
+    if (ok) avail |= 1u << k;
+    dd[k] = (CLOSEST && ok) ? depot_dist[bb * L + c] : __builtin_inff();
+  }
+  const float2* lrow = locs + bb * L;
+  const int64_t* prow = picklist + bb * (int64_t)O * K;
+  float2 xr[EPL];
+  int64_t pr[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const int c = sl + G * k;
+    xr[k] = c < L ? lrow[c] : make_float2(0.f, 0.f);
+    pr[k] = c < O * K ? prow[c] : 0;
   }
   bool range = false;
   for (int t = 0; t < P; ++t) {
@@ -344,12 +348,17 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
       int bi = 0x7fffffff;
 #pragma unroll
       for (int k = 0; k < EPL; ++k)
-        if (((avail >> k) & 1u) && dd[k] < best) {
+        if (dd[k] < best) {
           best = dd[k];
           bi = sl + G * k;
         }
-      grp_argmin<G>(best, bi);
+      grp_argmin_split<G>(best, bi);
       a64 = bi == 0x7fffffff ? 0 : bi;
+      if (bi != 0x7fffffff && sl == bi % G) {
+        const int slot = bi / G;
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) dd[k] = k == slot ? __builtin_inff() : dd[k];
+      }
       if (live && sl == 0) acts_out[(int64_t)t * B + bb] = a64;
     } else {
       a64 = acts_in[(int64_t)t * B + bb];
@@ -362,7 +371,20 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
       avail &= ~(1u << (int)(a / G));
     }
   }
-  __syncthreads();  // assignment rows and coordinates visible to the reward lanes
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const int c = sl + G * k;
+    if (c < L) xy[c] = xr[k];
+  }
+  // picklist entries as wrapped product indices (-1 = out of range)
+  for (int c = sl; c < O * K; c += G) {
+    int64_t pp = c < G * EPL ? pr[0] : prow[c];
+#pragma unroll
+    for (int k = 1; k < EPL; ++k) pp = (c == sl + G * k) ? pr[k] : pp;
+    if (pp < 0) pp += P;
+    pks[c] = (pp < 0 || pp >= P) ? -1 : (int32_t)pp;
+  }
+  __syncthreads();  // assignment rows, coordinates and picklist visible to the reward lanes
 
   for (int o = sl; o < O; o += G) {
     const int32_t* pk = pks + o * K;
