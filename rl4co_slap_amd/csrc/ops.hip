@@ -36,23 +36,48 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint8_t* src, int64_t
   if (__any(bad) && lane_id() == 0) set_status(status, CO_ST_INDEX_RANGE);
 }
 
-__global__ __launch_bounds__(256) void any_eq_kernel(const int64_t* x, int64_t n, int64_t value,
-                                                     int32_t* flag) {
-  bool hit = false;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
-    hit |= x[k] == value;
-  if (__any(hit) && lane_id() == 0) atomicOr(flag, 1);
+// One 1024-thread workgroup reduces the whole vector and writes the result itself: no
+// zeroing launch and no atomics (these feed per-step host polls inside graphs, where a
+// launch costs ~4-5 us of its own).  16-byte loads when the base is aligned.
+constexpr int kReduceThreads = 1024;
+
+__device__ __forceinline__ int block_sum_int(int v) {
+  __shared__ int s_part[kReduceThreads / 64];
+  v = wave_sum(v);
+  if (lane_id() == 0) s_part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int t = 0;
+  if (threadIdx.x < 64) {
+    t = threadIdx.x < kReduceThreads / 64 ? s_part[threadIdx.x] : 0;
+    t = wave_sum(t);
+  }
+  return t;  // valid in wave 0
 }
 
-__global__ __launch_bounds__(256) void count_not_done_kernel(const uint8_t* done, int64_t n,
-                                                             int32_t* count) {
+__global__ __launch_bounds__(kReduceThreads) void any_eq_kernel(const int64_t* x, int64_t n,
+                                                                int64_t value, int32_t* flag) {
+  int hit = 0;
+  for (int64_t k = threadIdx.x; k < n; k += kReduceThreads) hit |= x[k] == value;
+  hit = block_sum_int(hit);
+  if (threadIdx.x == 0) *flag = hit != 0;
+}
+
+__global__ __launch_bounds__(kReduceThreads) void count_not_done_kernel(const uint8_t* done,
+                                                                        int64_t n, int32_t* count) {
   int c = 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
-    c += done[k] == 0;
-  c = wave_sum(c);
-  if (lane_id() == 0 && c) atomicAdd(count, c);
+  const bool vec = (reinterpret_cast<uintptr_t>(done) & 15) == 0;
+  const int64_t n16 = vec ? (n & ~(int64_t)15) : 0;
+  for (int64_t k = (int64_t)threadIdx.x * 16; k < n16; k += (int64_t)kReduceThreads * 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(done + k);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c += ((w[q] >> (8 * j)) & 0xffu) == 0u;
+  }
+  for (int64_t k = n16 + threadIdx.x; k < n; k += kReduceThreads) c += done[k] == 0;
+  c = block_sum_int(c);
+  if (threadIdx.x == 0) *count = c;
 }
 
 // One wave per instance: lanes over the S starts (strided by `instances`).
@@ -139,23 +164,15 @@ extern "C" int co_gather_by_index(const void* src, int64_t outer, int64_t src_le
 
 extern "C" int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t* flag,
                              void* stream) {
-  if (n < 0 || !flag) return CO_E_INVAL;
-  const int e = zero_i32(flag, (hipStream_t)stream);
-  if (e != hipSuccess) return e;
-  if (n == 0) return CO_OK;
-  if (!x) return CO_E_INVAL;
-  hipLaunchKernelGGL(any_eq_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0,
-                     (hipStream_t)stream, x, n, value, flag);
+  if (n < 0 || !flag || (n > 0 && !x)) return CO_E_INVAL;
+  hipLaunchKernelGGL(any_eq_kernel, dim3(1), dim3(kReduceThreads), 0, (hipStream_t)stream, x, n,
+                     value, flag);
   return launch_status();
 }
 
 extern "C" int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream) {
-  if (n < 0 || !count) return CO_E_INVAL;
-  const int e = zero_i32(count, (hipStream_t)stream);
-  if (e != hipSuccess) return e;
-  if (n == 0) return CO_OK;
-  if (!done) return CO_E_INVAL;
-  hipLaunchKernelGGL(count_not_done_kernel, dim3(grid_for(n, 256, 1024)), dim3(256), 0,
+  if (n < 0 || !count || (n > 0 && !done)) return CO_E_INVAL;
+  hipLaunchKernelGGL(count_not_done_kernel, dim3(1), dim3(kReduceThreads), 0,
                      (hipStream_t)stream, done, n, count);
   return launch_status();
 }
