@@ -317,8 +317,8 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
     out["slap_fused_closest"] = {"value": world * b * 20 * 4 * k / t,
                                  "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
                                  "launch_us": ev / (4 * k) * 1e6,
-                                 "bytes_per_episode": 2834,
-                                 "achieved_GBps": b * 2834 / (ev / (4 * k)) / 1e9}
+                                 "bytes_per_episode": 2754,
+                                 "achieved_GBps": b * 2754 / (ev / (4 * k)) / 1e9}
     del fu
     if not stepwise:
         return out
