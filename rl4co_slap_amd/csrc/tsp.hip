@@ -68,6 +68,67 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
   mask_clear_tile<true>(B, N, action, mask_in, mask_out, status, vec != 0, epi);
 }
 
+// Lane-group step for rows of N % 4 == 0 bytes: G lanes per row, lane sl owns the
+// 4 mask words [4*sl, 4*sl + 4) of its row (u32 loads/stores); the action's byte is
+// cleared with a word select, the surviving entries are counted per word, done is a
+// group ballot, and the group's lane 0 writes the row scalars.  64/G rows per wave.
+#ifndef CO_TSP_STEP_GROUP
+#define CO_TSP_STEP_GROUP 1
+#endif
+template <int G>
+__global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
+                                                             const int64_t* __restrict__ action,
+                                                             const uint32_t* __restrict__ mask_in,
+                                                             uint32_t* __restrict__ mask_out,
+                                                             TspRowEpilogue epi, int first_mode,
+                                                             const int32_t* first_flag,
+                                                             int32_t* status) {
+  constexpr int WPL = 4;
+  const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
+  const int W = N >> 2;  // words per row
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+  if (first_mode == 2) epi.take_first = (*first_flag != 0);
+  for (int64_t base = wid * (64 / G); base < B; base += nwaves * (64 / G)) {
+    const int64_t b = base + lane / G;
+    const bool valid = b < B;
+    const int64_t r = valid ? b : 0;
+    const int64_t a_raw = action[r];
+    int64_t a = a_raw;
+    const typename TspRowEpilogue::Row rv = valid ? epi.load(r) : typename TspRowEpilogue::Row{};
+    const uint32_t* src = mask_in + r * W;
+    uint32_t w[WPL];
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+      const int c = sl * WPL + k;
+      w[k] = (valid && c < W) ? src[c] : 0u;
+    }
+    if (a < 0 || a >= N) {
+      if (valid && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
+      a = -1;
+    }
+    const int rel = (int)a - sl * WPL * 4;  // byte offset of the action in this lane's span
+    int left = 0;
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+      const uint32_t clr = (rel >= 4 * k && rel < 4 * k + 4) ? (0xffu << (8 * (rel - 4 * k))) : 0u;
+      w[k] &= ~clr;
+      // nonzero bytes of the word: high bit of each byte of (b & 0x7f) + 0x7f, or b
+      const uint32_t nz = (((w[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[k]) & 0x80808080u;
+      left += __builtin_popcount(nz);
+    }
+    uint32_t* dst = mask_out + r * W;
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+      const int c = sl * WPL + k;
+      if (valid && c < W) dst[c] = w[k];
+    }
+    const bool any_left = (__ballot(left != 0) & gmask) != 0;
+    if (valid && sl == 0) epi.store(r, a_raw, any_left ? 1 : 0, rv);
+  }
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void tsp_reward_kernel(int64_t B, int N, int T,
                                                                 const float2* locs, int64_t LB,
@@ -173,6 +234,27 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
   const int vec = tile_vec_ok(mask_in, mask_out);
   TspRowEpilogue epi{i_in, i_out, first_in, first_out, current_out, done, reward,
                      first_mode == 1};
+  if (CO_TSP_STEP_GROUP && (N & 3) == 0 && N <= 1024 &&
+      ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) & 3) == 0) {
+    const int W = (int)(N >> 2), G = W <= 8 ? 2 : W <= 16 ? 4 : W <= 32 ? 8 : W <= 64 ? 16
+                                                             : W <= 128 ? 32 : 64;
+    const int64_t waves = (B * G + 63) / 64;
+    const dim3 grid(grid_for(waves, 4, 256 * 32));
+    const uint32_t* mi = reinterpret_cast<const uint32_t*>(mask_in);
+    uint32_t* mo = reinterpret_cast<uint32_t*>(mask_out);
+    hipStream_t s = (hipStream_t)stream;
+#define CO_TSG(GG)                                                                             \
+  hipLaunchKernelGGL(tsp_step_group_kernel<GG>, grid, dim3(256), 0, s, B, (int)N, action, mi,  \
+                     mo, epi, first_mode, first_flag, status)
+    if (G == 2) CO_TSG(2);
+    else if (G == 4) CO_TSG(4);
+    else if (G == 8) CO_TSG(8);
+    else if (G == 16) CO_TSG(16);
+    else if (G == 32) CO_TSG(32);
+    else CO_TSG(64);
+#undef CO_TSG
+    return launch_status();
+  }
   const unsigned grid = (unsigned)((B + kTileRows - 1) / kTileRows);
   hipLaunchKernelGGL(tsp_step_kernel, dim3(grid), dim3(kTileThreads), 0, (hipStream_t)stream, B,
                      (int)N, action, mask_in, mask_out, epi, first_mode, first_flag, status, vec);
