@@ -40,14 +40,30 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile each source to an object in parallel, then link the shared library."""
+    from concurrent.futures import ThreadPoolExecutor
+
     if not force and not _stale():
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
+    obj_dir = os.path.join(OUT_DIR, "obj")
+    os.makedirs(obj_dir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+             "-fno-fast-math", "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include")]
+
+    def compile_one(src):
+        obj = os.path.join(obj_dir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc()] + flags + ["-c", os.path.join(HERE, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = min(len(SOURCES), max(1, min(os.cpu_count() or 1, 8)))
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-result",
-           "-I", os.path.join(ROOT, "include"), "-o", tmp]
-    cmd += [os.path.join(HERE, s) for s in SOURCES]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, "-x", "none"] + objs
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
