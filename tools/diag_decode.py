@@ -27,7 +27,7 @@ for B, N in [(102400, 100), (65536, 100), (102400, 20), (102400, 50), (16384, 20
     sr = torch.empty_like(done)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream().cuda_stream
-    for clip in ((0.0,) if os.environ.get("DIAG_QUICK") else (0.0, 10.0)):
+    for clip in ((float(os.environ.get("DIAG_CLIP", "0")),) if os.environ.get("DIAG_QUICK") else (0.0, 10.0)):
         for name in ("decode", "tsp_decode"):
             def run():
                 if name == "decode":
