@@ -283,6 +283,7 @@ def main():
         # instance generation, timed separately (SURVEY.md 8d protocol; 8f rank 1)
         modes["slap_generate_b16384"] = bench_generate_slap(args.slap_batch, dev,
                                                             with_ref=(rank == 0 and world == 1))
+        annotate_modes(modes, n, world)
         out["modes"] = modes
 
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -294,6 +295,31 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def annotate_modes(modes, n, world):
+    """Algorithmic HBM bytes per env-step of each mode (SURVEY.md 8d definitions; fused
+    modes: their kernels' own input/output bytes) -> per-GPU achieved
+    GB/s and the fraction of the 8 TB/s peak."""
+    per_step = {
+        "tsp_stepwise_graph": lambda m: 2 * n + 50 + (16 * n + 4) / n,
+        "tsp_fused_nearest": lambda m: (17 * n + 30) / n,
+        "slap_fused_closest": lambda m: 2754 / 20,
+        "slap_fused_closest_b65536": lambda m: 2754 / 20,
+        "slap_stepwise_graph": lambda m: 234 + 1684 / 20,
+        "pomo_tsp100": lambda m: 6 * n + 54,
+        "cvrp_fused_nearest": lambda m: (8 + 12 * n + 8 * m["episode_steps"] + 10 * (n + 1) + 25)
+        / m["episode_steps"],
+        "cvrp_stepwise_graph": lambda m: 7 * n + 33 + (16 * m["episode_steps"] + 12)
+        / m["episode_steps"],
+    }
+    for name, f in per_step.items():
+        if name in modes and "value" in modes[name]:
+            m = modes[name]
+            byts = f(m)
+            gbs = m["value"] / world * byts / 1e9
+            m.update({"alg_bytes_per_env_step": byts, "achieved_GBps_per_gpu": gbs,
+                      "hbm_frac": gbs / HBM_PEAK_GBS})
 
 
 def bench_slap(b, k, world, rank, dev, stepwise=True):
