@@ -7,7 +7,7 @@ assertion (``decoding.py:376-379,393-395``) is recorded in a device status word
 and raised once in ``post_decoder_hook`` instead of synchronising every step.
 Top-k / top-p filtering runs inside the same launch (``co_decode_step_ex``); beam search
 ranks the beams' candidates with ``co_beam_select`` and re-indexes the state rows with
-the device gather.  Multi-sampling is out of scope.
+the device gather.
 """
 from __future__ import annotations
 
@@ -210,6 +210,13 @@ class Sampling(DecodingStrategy):
         return "sampling"
 
 
+class MultiSampling(Sampling):
+    """``decoding.py:421-472``: sampling (with ``multisample=True`` the td is batchified
+    ``num_starts`` times in ``pre_decoder_hook`` without start-node selection)."""
+
+    name = "multisampling"
+
+
 class Evaluate(DecodingStrategy):
     name = "evaluate"
 
@@ -339,9 +346,10 @@ class BeamSearch(DecodingStrategy):
 
 
 def get_decoding_strategy(decoding_strategy, **config):
-    """``decoding.py:17-36`` (multisampling is out of scope)."""
+    """``decoding.py:17-36``."""
     registry = {"greedy": Greedy, "sampling": Sampling, "multistart_greedy": Greedy,
-                "multistart_sampling": Sampling, "evaluate": Evaluate, "beam_search": BeamSearch}
+                "multistart_sampling": Sampling, "evaluate": Evaluate, "beam_search": BeamSearch,
+                "multisampling": MultiSampling}
     if "multistart" in decoding_strategy:
         config["multistart"] = True
     return registry.get(decoding_strategy, Sampling)(**config)

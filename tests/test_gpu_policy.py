@@ -86,3 +86,21 @@ def test_policy_beam_search_matches_oracle(dev, name, b, n, bw, select_best):
     assert ((r - rr).abs() <= 1e-5 * rr.abs().clamp(min=1)).all()
     ll, lr = out["log_likelihood"].cpu(), ref["log_likelihood"]
     assert ((ll - lr).abs() <= 1e-4 * lr.abs().clamp(min=1)).all()
+
+
+def test_policy_multisampling(dev):
+    """decode_type="multisampling" with multisample=True: the td is batchified num_starts
+    times without start-node selection (decoding.py:271-313) and every sample is a
+    valid tour; select_best keeps the best sample per instance."""
+    b, n, s = 16, 20, 4
+    _, _, env, td = _pair("tsp", b, n, 7, dev)
+    pol = ConstructivePolicy(None, LogitsDecoder(neg_dist_logits), env_name="tsp")
+    out = pol(td, env, decode_type="multisampling", multisample=True, num_starts=s,
+              return_actions=True)
+    a = out["actions"]
+    assert a.shape == (s * b, n)
+    assert torch.equal(a.sort(1).values.cpu(), torch.arange(n).expand(s * b, n))
+    _, _, env2, td2 = _pair("tsp", b, n, 7, dev)
+    best = pol(td2, env2, decode_type="multisampling", multisample=True, num_starts=s,
+               select_best=True, return_actions=True)
+    assert best["actions"].shape == (b, n) and best["reward"].shape == (b,)
