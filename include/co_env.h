@@ -313,6 +313,11 @@ int co_beam_select(int64_t batch, int64_t beam_width, int64_t n_actions, const f
                    int64_t* selected, int32_t* beam_parent, int64_t* beam_row,
                    float* score_out, int32_t* status, void* stream);
 
+/* get_distance_matrix (rl4co/utils/ops.py:104-111): out[B, N, N] = Euclidean distances
+ * between the instance's coordinates, f32 sqrt(dx*dx + dy*dy).  out 16-byte aligned. */
+int co_distance_matrix(int64_t batch, int64_t num_loc, const float* locs, float* out,
+                       void* stream);
+
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 

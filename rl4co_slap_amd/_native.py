@@ -41,6 +41,7 @@ _SIGS = {
     "co_decode_step_ex": [_i64, _i64, _p, _i64, _p, _f32, _f32, _i32, _f64, _i32, _p, _p, _p, _p,
                           _u64, _u64, _p, _p],
     "co_beam_select": [_i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
+    "co_distance_matrix": [_i64, _i64, _p, _p, _p],
     "co_tsp_nearest_action": [_i64, _i64, _p, _p, _p, _i32, _p, _p],
     "co_cvrp_nearest_action": [_i64, _i64, _p, _p, _p, _p, _p],
     "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],

@@ -244,3 +244,51 @@ extern "C" int co_symmetric_augment(int64_t B, int64_t N, const float* xy, const
                      reinterpret_cast<float2*>(out));
   return launch_status();
 }
+
+// utils/ops.py:104-111 get_distance_matrix: out[b, i, j] = |locs[b,i] - locs[b,j]|_2 in
+// f32 (sqrt(dx*dx + dy*dy), correctly rounded).  Four j per thread, float4 stores when
+// N % 4 == 0; the instance's coordinates come from L2 after the first touch.
+namespace {
+__global__ __launch_bounds__(256) void distance_matrix_kernel(int64_t B, int N,
+                                                              const float2* __restrict__ locs,
+                                                              float* __restrict__ out) {
+  const int64_t NN = (int64_t)N * N;
+  const bool vec = (N & 3) == 0;
+  const int64_t units = vec ? B * (NN / 4) : B * NN;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = vec ? u * 4 : u;
+    const int64_t b = e / NN, r = e - b * NN;
+    const int i = (int)(r / N), j = (int)(r - (int64_t)i * N);
+    const float2* row = locs + b * N;
+    const float2 p = row[i];
+    if (vec) {
+      float d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float2 o = row[j + q];
+        const float dx = p.x - o.x, dy = p.y - o.y;
+        d[q] = sqrtf(dx * dx + dy * dy);
+      }
+      *reinterpret_cast<float4*>(out + e) = make_float4(d[0], d[1], d[2], d[3]);
+    } else {
+      const float2 o = row[j];
+      const float dx = p.x - o.x, dy = p.y - o.y;
+      out[e] = sqrtf(dx * dx + dy * dy);
+    }
+  }
+}
+}  // namespace
+
+extern "C" int co_distance_matrix(int64_t B, int64_t N, const float* locs, float* out,
+                                  void* stream) {
+  if (B < 0 || N <= 0 || N > (1 << 15)) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!locs || !out) return CO_E_INVAL;
+  if ((reinterpret_cast<uintptr_t>(locs) & 7) || (reinterpret_cast<uintptr_t>(out) & 15))
+    return CO_E_ALIGN;
+  hipLaunchKernelGGL(distance_matrix_kernel, dim3(grid_for(B * N * N / 4 + 1, 256, 16384)),
+                     dim3(256), 0, (hipStream_t)stream, B, (int)N,
+                     reinterpret_cast<const float2*>(locs), out);
+  return launch_status();
+}

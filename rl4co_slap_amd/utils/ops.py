@@ -119,6 +119,18 @@ def get_tour_length(ordered_locs: Tensor) -> Tensor:
     return -out
 
 
+def get_distance_matrix(locs: Tensor) -> Tensor:
+    """``ops.py:104-111``: ``[..., N, 2] -> [..., N, N]`` Euclidean distances (gfx950
+    kernel, one launch)."""
+    nat.require_device(locs)
+    lead, n = locs.shape[:-2], locs.shape[-2]
+    flat = locs.reshape(-1, n, 2).contiguous().float()
+    out = torch.empty((flat.shape[0], n, n), dtype=torch.float32, device=locs.device)
+    nat.call("co_distance_matrix", flat.shape[0], n, nat.ptr(flat), nat.ptr(out),
+             nat.stream_of(flat))
+    return out.reshape(*lead, n, n)
+
+
 def get_num_starts(td, env_name=None):
     """``ops.py:126-136``."""
     n = td["action_mask"].shape[-1]

@@ -206,3 +206,15 @@ def test_decode_top_k_duplicates_and_sampling(dev):
         a, _, _ = decode_step(logits.to(dev), mask.to(dev), "sampling", top_k=4, seed=5,
                               offset=off)
         assert keep.gather(1, a.cpu()[:, None]).all()
+
+
+@pytest.mark.parametrize("shape", [(3, 20), (2, 5, 7), (64, 100)])
+def test_distance_matrix(dev, shape):
+    from rl4co_slap_amd.utils.ops import get_distance_matrix
+
+    locs = torch.rand(*shape, 2)
+    want = (locs[..., :, None, :] - locs[..., None, :, :]).norm(p=2, dim=-1)  # ops.py:110
+    got = get_distance_matrix(locs.to(dev)).cpu()
+    assert got.shape == want.shape
+    assert torch.allclose(got, want, rtol=2e-7, atol=1e-7)
+    assert (got.diagonal(dim1=-2, dim2=-1) == 0).all()
