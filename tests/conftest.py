@@ -31,5 +31,10 @@ def dev():
 
     if os.environ.get("CO_TEST_LIB"):  # a tuning variant (tools/build_variants.sh)
         _native.LIB_PATH = os.environ["CO_TEST_LIB"]
-    _native.load()  # fail loudly if the library is missing
+    else:  # test infrastructure builds a missing / stale in-tree library; the product
+        # itself never builds and fails loudly without it
+        from rl4co_slap_amd.csrc.build import build
+
+        build(force=False)
+    _native.load()
     return torch.device("cuda:0")
