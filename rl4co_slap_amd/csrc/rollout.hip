@@ -42,13 +42,16 @@ __device__ __forceinline__ void stage_bytes_lds(const unsigned char* __restrict_
   __syncthreads();
 }
 
-// A row of visited bits -> n mask bytes (1 = still feasible) at `row` in LDS (dword
-// writes when n % 4 == 0: conflict-free for odd n/4).
+// Columns [c_lo, c_hi) of a row of visited bits -> mask bytes (1 = still feasible) of
+// `row` in LDS (dword writes when n % 4 == 0 and c_lo % 4 == 0: conflict-free for odd
+// n/4).
 template <int NW>
 __device__ __forceinline__ void mask_row_to_lds(const uint64_t (&m)[NW], int n,
-                                                unsigned char* row) {
-  if ((n & 3) == 0) {
-    for (int c = 0; c < n; c += 4) {
+                                                unsigned char* row, int c_lo = 0,
+                                                int c_hi = -1) {
+  if (c_hi < 0) c_hi = n;
+  if ((n & 3) == 0 && (c_lo & 3) == 0) {
+    for (int c = c_lo; c < c_hi; c += 4) {
       uint32_t v = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -62,7 +65,7 @@ __device__ __forceinline__ void mask_row_to_lds(const uint64_t (&m)[NW], int n,
       *reinterpret_cast<uint32_t*>(row + c) = v;
     }
   } else {
-    for (int c = 0; c < n; ++c) {
+    for (int c = c_lo; c < c_hi; ++c) {
       uint64_t w = 0;
 #pragma unroll
       for (int k = 0; k < NW; ++k)
@@ -257,7 +260,12 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
   uint64_t m[NW];
 #pragma unroll
   for (int kk = 0; kk < NW; ++kk) m[kk] = (uint64_t)vw[2 * kk] | ((uint64_t)vw[2 * kk + 1] << 32);
-  if (STATE && q == 0 && live) mask_row_to_lds<NW>(m, N, smem + (size_t)lane * N);
+  if (STATE && live) {  // the Q waves expand column quarters of the lane's mask row
+    const int per = ((N + 4 * Q - 1) / (4 * Q)) * 4;
+    const int c_lo = q * per < N ? q * per : N;
+    const int c_hi = c_lo + per < N ? c_lo + per : N;
+    mask_row_to_lds<NW>(m, N, smem + (size_t)lane * N, c_lo, c_hi);
+  }
   __syncthreads();
   if (q == 0 && live) {
     double tot = 0.0;
