@@ -392,7 +392,11 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
     if (pp < 0) pp += P;
     pks[c] = (pp < 0 || pp >= P) ? -1 : (int32_t)pp;
   }
-  __syncthreads();  // assignment rows, coordinates and picklist visible to the reward lanes
+  // the group's LDS rows are written and read by lanes of the same wave: a wave-level
+  // fence orders them, no workgroup barrier (groups do not wait for other waves)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
   for (int o = sl; o < O; o += G) {
     const int32_t* pk = pks + o * K;
@@ -422,7 +426,9 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
     len += edge_len(prev.x, prev.y, p0.x, p0.y);
     olen[o] = len;
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
   if (live) {
     uint8_t* mrow = mask_out + bb * L;
