@@ -31,21 +31,31 @@ using namespace co;
 #ifndef CO_DECODE_UNR
 #define CO_DECODE_UNR 1
 #endif
+__device__ __forceinline__ float co_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// tanh(x) = 1 - 2 / (e^{2x} + 1) on v_exp / v_rcp (abs error ~1e-7, exact +-1 saturation)
+__device__ __forceinline__ float co_tanh_fast(float x) {
+  const float e = co_exp2(x * 2.8853900817779268f);  // e^{2x}
+  return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
+}
+__device__ __forceinline__ float co_exp_fast(float x) { return co_exp2(x * 1.4426950408889634f); }
+
 #ifndef CO_FAST_EXP
 #define CO_FAST_EXP 1  // hardware v_exp_f32 in the softmax sums (<= 2 ulp; logp parity is 1e-5)
 #endif
 #if CO_FAST_EXP
-#define CO_EXPF __expf
+#define CO_EXPF co_exp_fast
 #else
 #define CO_EXPF expf
+#endif
+#ifndef CO_GREEDY_FAST
+#define CO_GREEDY_FAST 1  // greedy rows on GreedyRow (first index at the max logp)
 #endif
 #ifndef CO_FAST_TANH
 #define CO_FAST_TANH 1
 #endif
 #if CO_FAST_TANH
-// 1 - 2 / (e^(2x) + 1) on the hardware exp: absolute error ~1e-7 (saturates exactly to
-// +-1), against ~25 instructions for the libm tanhf
-__device__ __forceinline__ float co_tanhf(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
+// against ~25 instructions for the libm tanhf
+__device__ __forceinline__ float co_tanhf(float x) { return co_tanh_fast(x); }
 #else
 __device__ __forceinline__ float co_tanhf(float x) { return tanhf(x); }
 #endif
@@ -294,6 +304,140 @@ struct DecodeRow {
   }
 };
 
+// ---------------------------------------------------------------------------
+// Greedy row engine (decoding.py:327-335: argmax of log_softmax, first index on ties).
+// The max log-probability of a row is exactly fl(0 - L) (L = log of the exp-sum, the
+// max element has x - m = 0) and every logp = fl((x - m) - L) is monotone in x, so the
+// greedy action is the first index whose logp equals fl(0 - L): one subtract + compare
+// per element and an integer group min, instead of a (value, index) argmax butterfly, and
+// the selected log-probability needs no broadcast.  Same association and exp sums as
+// DecodeRow, so actions and logp are the bits DecodeRow produces.  A row whose L is not
+// finite (every action masked, a NaN / +inf logit) has NaN log-probabilities throughout:
+// index 0 (torch.argmax picks the first NaN), logp NaN.  The mask is kept as 4-byte
+// words (pad slots past N read as masked); VEC loads them as they lie (N % 4 == 0),
+// otherwise they are assembled from byte loads.
+template <int RL, int EPL, bool VEC>
+struct GreedyRow {
+  static_assert(EPL % 4 == 0, "GreedyRow keeps the mask in u32 words");
+  float v[EPL];
+  uint32_t mw[EPL / 4];
+
+  __device__ __forceinline__ void load(bool valid, int N, const float* lrow, const uint8_t* mrow,
+                                       int c0) {
+#pragma unroll
+    for (int j = 0; j < EPL / 4; ++j) {
+      const int c = c0 + 4 * j;
+      if (VEC) {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint32_t mm = 0u;
+        if (valid && c < N) {
+          x = *reinterpret_cast<const float4*>(lrow + c);
+          mm = mrow ? *reinterpret_cast<const uint32_t*>(mrow + c) : 0x01010101u;
+        }
+        v[4 * j] = x.x;
+        v[4 * j + 1] = x.y;
+        v[4 * j + 2] = x.z;
+        v[4 * j + 3] = x.w;
+        mw[j] = mm;
+      } else {
+        uint32_t mm = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool in = valid && c + q < N;
+          v[4 * j + q] = in ? lrow[c + q] : 0.f;
+          const uint32_t b = in ? (mrow ? (uint32_t)mrow[c + q] : 1u) : 0u;
+          mm |= b << (8 * q);
+        }
+        mw[j] = mm;
+      }
+    }
+  }
+
+  __device__ __forceinline__ bool allowed(int k) const {
+    return ((mw[k >> 2] >> (8 * (k & 3))) & 0xffu) != 0u;
+  }
+
+  // leaves v[k] = x_k - m; returns L (NaN for the degenerate rows above)
+  __device__ __forceinline__ float softmax_shift(float clip, float temp) {
+    const float NEG_INF = -__builtin_inff();
+    float m = NEG_INF;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      float t = v[k];
+      if (clip > 0.f) t = co_tanhf(t) * clip;
+      if (temp != 1.f) t = t / temp;
+      t = allowed(k) ? t : NEG_INF;
+      v[k] = t;
+      m = fmaxf(m, t);
+    }
+    m = grp_max<RL>(m);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const float d = v[k] - m;
+      v[k] = d;
+      s += CO_EXPF(d);
+    }
+    s = grp_sum<RL>(s);
+    return logf(s);
+  }
+
+  // greedy action of the row (valid on every lane of the group) and its logp
+  __device__ __forceinline__ int select(float L, int c0, float& lp) const {
+    lp = 0.f - L;
+    int idx = 0x7fffffff;
+#pragma unroll
+    for (int k = EPL - 1; k >= 0; --k) idx = (v[k] - L == lp) ? c0 + k : idx;
+    idx = grp_min_int<RL>(idx);
+    return idx == 0x7fffffff ? 0 : idx;  // no match only when L is NaN: all logp NaN
+  }
+};
+
+template <int RL, int EPL, bool VEC>
+__global__ __launch_bounds__(256) void decode_greedy_kernel(
+    int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
+    const uint8_t* __restrict__ mask, float clip, float temp, int64_t* __restrict__ action_out,
+    float* __restrict__ logp_sel, float* __restrict__ full, int32_t* status) {
+  constexpr int RPW = 64 / RL;
+  const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+    const int64_t row = base + grp;
+    const bool valid = row < B;
+    const int64_t r = valid ? row : 0;
+    GreedyRow<RL, EPL, VEC> g;
+    g.load(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, c0);
+    const float L = g.softmax_shift(clip, temp);
+    float lp;
+    const int sel = g.select(L, c0, lp);
+    if (!valid) continue;
+    if (full) {
+      float* frow = full + r * (int64_t)N + c0;
+#pragma unroll
+      for (int j = 0; j < EPL / 4; ++j) {
+        if (VEC) {
+          if (c0 + 4 * j < N)
+            *reinterpret_cast<float4*>(frow + 4 * j) =
+                make_float4(g.v[4 * j] - L, g.v[4 * j + 1] - L, g.v[4 * j + 2] - L,
+                            g.v[4 * j + 3] - L);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (c0 + 4 * j + q < N) frow[4 * j + q] = g.v[4 * j + q] - L;
+        }
+      }
+    }
+    if (sl == 0) {
+      // L is finite or NaN (the exp-sum is >= 1 unless NaN); finite means the argmax
+      // element is unmasked, NaN means index 0 was taken
+      if (mask && L != L && !g.allowed(0)) set_status(status, CO_ST_INFEASIBLE);
+      action_out[r] = sel;
+      if (logp_sel) logp_sel[r] = lp;
+    }
+  }
+}
+
 template <int RL, int EPL, bool VEC>
 __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const float* logits,
                                                      int64_t lstride, const uint8_t* mask,
@@ -411,6 +555,73 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
   }
 }
 
+// Greedy decode step fused with TSPEnv._step on the GreedyRow engine (the POMO /
+// multistart-greedy hot loop); same outputs as tsp_decode_step_kernel in greedy mode.
+// The mask words are updated in registers (the selected byte cleared) and stored back.
+template <int RL, int EPL, bool VEC>
+__global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
+    int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
+    const uint8_t* __restrict__ mask_in, float clip, float temp, int64_t* __restrict__ action_out,
+    float* __restrict__ logp_sel, uint8_t* __restrict__ mask_out, const int64_t* __restrict__ i_in,
+    int64_t* __restrict__ i_out, const int64_t* __restrict__ first_in,
+    int64_t* __restrict__ first_out, int take_first, uint8_t* __restrict__ done,
+    uint8_t* __restrict__ step_reward, float* __restrict__ ll_accum, int32_t* status) {
+  constexpr int RPW = 64 / RL;
+  const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
+  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+    const int64_t row = base + grp;
+    const bool valid = row < B;
+    const int64_t r = valid ? row : 0;
+    int64_t iv = 0, fv = 0;
+    float acc = 0.f;
+    if (valid && sl == 0) {
+      iv = i_in[r];
+      if (!take_first) fv = first_in[r];
+      if (ll_accum) acc = ll_accum[r];
+    }
+    GreedyRow<RL, EPL, VEC> g;
+    g.load(valid, N, logits + r * lstride, mask_in + r * (int64_t)N, c0);
+    const float L = g.softmax_shift(clip, temp);
+    float lp;
+    const int sel = g.select(L, c0, lp);
+    const bool feas0 = g.allowed(0);
+    uint32_t left = 0u;
+#pragma unroll
+    for (int j = 0; j < EPL / 4; ++j) {
+      const int off = sel - (c0 + 4 * j);
+      if ((unsigned)off < 4u) g.mw[j] &= ~(0xffu << (8 * off));
+      left |= g.mw[j];
+    }
+    if (valid) {
+      uint8_t* orow = mask_out + r * (int64_t)N + c0;
+#pragma unroll
+      for (int j = 0; j < EPL / 4; ++j) {
+        if (VEC) {
+          if (c0 + 4 * j < N) *reinterpret_cast<uint32_t*>(orow + 4 * j) = g.mw[j];
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (c0 + 4 * j + q < N) orow[4 * j + q] = (uint8_t)(g.mw[j] >> (8 * q));
+        }
+      }
+    }
+    const bool any_left = (__ballot(left != 0u) & gmask) != 0;
+    if (valid && sl == 0) {
+      if (L != L && !feas0) set_status(status, CO_ST_INFEASIBLE);
+      action_out[r] = sel;
+      if (logp_sel) logp_sel[r] = lp;
+      if (ll_accum) ll_accum[r] = acc + lp;  // get_log_likelihood's sum, per step
+      i_out[r] = iv + 1;
+      first_out[r] = take_first ? (int64_t)sel : fv;
+      done[r] = !any_left;
+      step_reward[r] = 0;
+    }
+  }
+}
+
 // RL lanes x EPL consecutive elements per row, by row-length bucket (CO_RL* above).
 #define CO_ROW_DISPATCH(LAUNCH, V)                           \
   if (N <= 16) LAUNCH(CO_RL16, 16 / CO_RL16, V);             \
@@ -449,6 +660,20 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
   if (mode == CO_DECODE_EVALUATE && !action_in) return CO_E_INVAL;
   const dim3 grid(decode_grid(B, (int)N)), block(256);
   hipStream_t s = (hipStream_t)stream;
+  const bool filtered = (top_k > 0 && top_k < N) || (top_p > 0.0 && top_p < 1.0);
+  if (CO_GREEDY_FAST && mode == CO_DECODE_GREEDY && !filtered) {
+#define CO_GREEDY(RL, EPL, V)                                                                  \
+  hipLaunchKernelGGL((decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V>), grid, block, 0, s, B,  \
+                     (int)N, logits, lstride, mask, clip, temp, action_out, logp_sel, full,     \
+                     status)
+    if (decode_vec_ok(logits, lstride, mask, N) && (reinterpret_cast<uintptr_t>(full) & 15) == 0) {
+      CO_ROW_DISPATCH(CO_GREEDY, true);
+    } else {
+      CO_ROW_DISPATCH(CO_GREEDY, false);
+    }
+#undef CO_GREEDY
+    return launch_status();
+  }
 #define CO_DECODE(RL, EPL, V)                                                                  \
   hipLaunchKernelGGL((decode_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N, logits,        \
                      lstride, mask, clip, temp, mode, action_in, action_out, logp_sel, full,   \
@@ -486,8 +711,24 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
       !done || !step_reward || (first_mode == 0 && !first_in) ||
       (mode == CO_DECODE_EVALUATE && !action_in))
     return CO_E_INVAL;
-  const dim3 grid(decode_grid(B, (int)N, CO_DECODE_UNR)), block(256);
   hipStream_t s = (hipStream_t)stream;
+  if (CO_GREEDY_FAST && mode == CO_DECODE_GREEDY) {
+    const dim3 grid(decode_grid(B, (int)N)), block(256);
+#define CO_TDG(RL, EPL, V)                                                                     \
+  hipLaunchKernelGGL((tsp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V>), grid, block, 0, s, \
+                     B, (int)N, logits, lstride, mask_in, clip, temp, action_out, logp_sel,     \
+                     mask_out, i_in, i_out, first_in, first_out, first_mode, done, step_reward, \
+                     ll_accum, status)
+    if (decode_vec_ok(logits, lstride, mask_in, N) &&
+        (reinterpret_cast<uintptr_t>(mask_out) & 3) == 0) {
+      CO_ROW_DISPATCH(CO_TDG, true);
+    } else {
+      CO_ROW_DISPATCH(CO_TDG, false);
+    }
+#undef CO_TDG
+    return launch_status();
+  }
+  const dim3 grid(decode_grid(B, (int)N, CO_DECODE_UNR)), block(256);
 #define CO_TDS(RL, EPL, V)                                                                     \
   hipLaunchKernelGGL((tsp_decode_step_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N,       \
                      logits, lstride, mask_in, clip, temp, mode, action_in, action_out,        \

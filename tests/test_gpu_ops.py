@@ -102,6 +102,38 @@ def test_decode_greedy_exact_ties(dev):
     assert torch.equal(act.cpu(), ref)
 
 
+@pytest.mark.parametrize("n", [100, 50])
+def test_decode_greedy_rounding_ties(dev, n):
+    # distinct logits whose log-probabilities round to the same float: the greedy action is
+    # the first index at the maximal logp (argmax of the logp row), not the largest logit
+    b = 256
+    g = torch.Generator().manual_seed(5)
+    logits = torch.zeros(b, n)
+    j0 = torch.randint(0, n - 1, (b,), generator=g)
+    eps = torch.rand(b, generator=g) * 4e-7  # below half an ulp of L = log(n) for most rows
+    rows = torch.arange(b)
+    logits[rows, j0 + 1] = eps  # the larger logit sits after the smaller one
+    mask = torch.ones(b, n, dtype=torch.bool)
+    act, lp, full = decode_step(logits.to(dev), mask.to(dev), "greedy", return_full=True)
+    full, act, lp = full.cpu(), act.cpu(), lp.cpu()
+    assert torch.equal(act, full.argmax(-1))  # torch.argmax: first maximal index
+    assert torch.equal(lp, full.gather(1, act[:, None]).squeeze(1))
+    assert (act < (j0 + 1)).any()  # some rows resolve to an earlier, smaller logit
+    # evaluate re-scores the selected actions to the same bits
+    ev_act, ev_lp, _ = decode_step(logits.to(dev), mask.to(dev), "evaluate", action=act.to(dev))
+    assert torch.equal(ev_lp.cpu(), lp)
+
+
+def test_decode_greedy_nan_row(dev):
+    logits = torch.randn(8, 12)
+    logits[3, 5] = float("nan")
+    mask = torch.ones(8, 12, dtype=torch.bool)
+    act, lp, _ = decode_step(logits.to(dev), mask.to(dev), "greedy")
+    ref = odec.process_logits(logits, mask)
+    assert torch.equal(act.cpu(), ref.argmax(-1))
+    assert torch.isnan(lp[3]).item() and torch.isfinite(lp.cpu()[torch.arange(8) != 3]).all()
+
+
 def test_decode_infeasible_flag(dev):
     from rl4co_slap_amd import _native as nat
 
