@@ -92,8 +92,8 @@ __device__ __forceinline__ uint32_t philox_u32(uint64_t seed, uint64_t offset, u
 // Lane `sl` of the group owns the EPL consecutive elements c = sl*EPL + k.  VEC: the
 // row's logits are read as float4 and its mask bytes as u32 (needs N % 4 == 0 and a
 // 16-byte aligned logits row stride); otherwise scalar loads.
-template <int RL, int EPL, bool VEC>
-struct DecodeRow {
+template <int RL, int EPL, bool VEC, int OPT>
+struct DecodeRow {  // OPT: clip / temperature flags as in GreedyRow::softmax_shift
   float x[EPL];     // log-probabilities after `run`
   uint8_t mk[EPL];  // the row's action_mask bytes (1 when no mask)
   int sel;          // selected action (valid on every lane of the group)
@@ -226,9 +226,9 @@ struct DecodeRow {
       float v = NEG_INF;
       if (valid && c0 + k < N) {
         v = x[k];
-        if (clip > 0.f) v = co_tanhf(v) * clip;
+        if (OPT & 1) v = co_tanhf(v) * clip;
         if (!mk[k]) v = NEG_INF;
-        if (temp != 1.f) v = v / temp;  // x / 1 == x exactly: skip the IEEE divide
+        if (OPT & 2) v = v / temp;  // x / 1 == x exactly: skip the IEEE divide
         m = fmaxf(m, v);
       }
       x[k] = v;
@@ -314,9 +314,27 @@ struct DecodeRow {
 // DecodeRow, so actions and logp are the bits DecodeRow produces.  A row whose L is not
 // finite (every action masked, a NaN / +inf logit) has NaN log-probabilities throughout:
 // index 0 (torch.argmax picks the first NaN), logp NaN.  The mask is kept as 4-byte
-// words (pad slots past N read as masked); VEC loads them as they lie (N % 4 == 0),
-// otherwise they are assembled from byte loads.
-template <int RL, int EPL, bool VEC>
+// words (pad slots past N read as masked).  VW = elements per load: 4 (float4 + u32 mask,
+// N % 4 == 0), 2 (float2 + u16, N even) or 1.
+template <int VW>
+struct Chunk;
+template <>
+struct Chunk<4> {
+  using F = float4;
+  using M = uint32_t;
+};
+template <>
+struct Chunk<2> {
+  using F = float2;
+  using M = uint16_t;
+};
+template <>
+struct Chunk<1> {
+  using F = float;
+  using M = uint8_t;
+};
+
+template <int RL, int EPL, int VW>
 struct GreedyRow {
   static_assert(EPL % 4 == 0, "GreedyRow keeps the mask in u32 words");
   float v[EPL];
@@ -324,33 +342,57 @@ struct GreedyRow {
 
   __device__ __forceinline__ void load(bool valid, int N, const float* lrow, const uint8_t* mrow,
                                        int c0) {
+    using F = typename Chunk<VW>::F;
+    using M = typename Chunk<VW>::M;
 #pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {
-      const int c = c0 + 4 * j;
-      if (VEC) {
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        uint32_t mm = 0u;
-        if (valid && c < N) {
-          x = *reinterpret_cast<const float4*>(lrow + c);
-          mm = mrow ? *reinterpret_cast<const uint32_t*>(mrow + c) : 0x01010101u;
-        }
-        v[4 * j] = x.x;
-        v[4 * j + 1] = x.y;
-        v[4 * j + 2] = x.z;
-        v[4 * j + 3] = x.w;
-        mw[j] = mm;
-      } else {
-        uint32_t mm = 0u;
+      uint32_t mm = 0u;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool in = valid && c + q < N;
-          v[4 * j + q] = in ? lrow[c + q] : 0.f;
-          const uint32_t b = in ? (mrow ? (uint32_t)mrow[c + q] : 1u) : 0u;
-          mm |= b << (8 * q);
+      for (int h = 0; h < 4 / VW; ++h) {
+        const int c = c0 + 4 * j + VW * h;
+        F x;
+        uint32_t m = 0u;
+        if (valid && c < N) {
+          x = *reinterpret_cast<const F*>(lrow + c);
+          m = mrow ? (uint32_t) * reinterpret_cast<const M*>(mrow + c) : (0x01010101u >> (32 - 8 * VW));
+        } else {
+          x = F{};
         }
-        mw[j] = mm;
+        const float* xf = reinterpret_cast<const float*>(&x);
+#pragma unroll
+        for (int q = 0; q < VW; ++q) v[4 * j + VW * h + q] = xf[q];
+        mm |= m << (8 * VW * h);
       }
+      mw[j] = mm;
     }
+  }
+
+  // the row's mask words / logp values back to memory (pad chunks skipped)
+  __device__ __forceinline__ void store_mask(int N, uint8_t* orow, int c0) const {
+    using M = typename Chunk<VW>::M;
+#pragma unroll
+    for (int j = 0; j < EPL / 4; ++j)
+#pragma unroll
+      for (int h = 0; h < 4 / VW; ++h) {
+        const int c = c0 + 4 * j + VW * h;
+        if (c < N) *reinterpret_cast<M*>(orow + c) = (M)(mw[j] >> (8 * VW * h));
+      }
+  }
+  __device__ __forceinline__ void store_logp(int N, float L, float* frow, int c0) const {
+    using F = typename Chunk<VW>::F;
+#pragma unroll
+    for (int j = 0; j < EPL / 4; ++j)
+#pragma unroll
+      for (int h = 0; h < 4 / VW; ++h) {
+        const int c = c0 + 4 * j + VW * h;
+        if (c < N) {
+          F x;
+          float* xf = reinterpret_cast<float*>(&x);
+#pragma unroll
+          for (int q = 0; q < VW; ++q) xf[q] = v[4 * j + VW * h + q] - L;
+          *reinterpret_cast<F*>(frow + c) = x;
+        }
+      }
   }
 
   __device__ __forceinline__ bool allowed(int k) const {
@@ -358,14 +400,17 @@ struct GreedyRow {
   }
 
   // leaves v[k] = x_k - m; returns L (NaN for the degenerate rows above)
+  // OPT bit 0: tanh clipping, bit 1: temperature != 1 (template flags: as runtime
+  // conditions the compiler evaluates both arms per element and selects)
+  template <int OPT>
   __device__ __forceinline__ float softmax_shift(float clip, float temp) {
     const float NEG_INF = -__builtin_inff();
     float m = NEG_INF;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
       float t = v[k];
-      if (clip > 0.f) t = co_tanhf(t) * clip;
-      if (temp != 1.f) t = t / temp;
+      if (OPT & 1) t = co_tanhf(t) * clip;
+      if (OPT & 2) t = t / temp;
       t = allowed(k) ? t : NEG_INF;
       v[k] = t;
       m = fmaxf(m, t);
@@ -393,7 +438,7 @@ struct GreedyRow {
   }
 };
 
-template <int RL, int EPL, bool VEC>
+template <int RL, int EPL, int VW, int OPT>
 __global__ __launch_bounds__(256) void decode_greedy_kernel(
     int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask, float clip, float temp, int64_t* __restrict__ action_out,
@@ -406,28 +451,13 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
-    GreedyRow<RL, EPL, VEC> g;
+    GreedyRow<RL, EPL, VW> g;
     g.load(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, c0);
-    const float L = g.softmax_shift(clip, temp);
+    const float L = g.template softmax_shift<OPT>(clip, temp);
     float lp;
     const int sel = g.select(L, c0, lp);
     if (!valid) continue;
-    if (full) {
-      float* frow = full + r * (int64_t)N + c0;
-#pragma unroll
-      for (int j = 0; j < EPL / 4; ++j) {
-        if (VEC) {
-          if (c0 + 4 * j < N)
-            *reinterpret_cast<float4*>(frow + 4 * j) =
-                make_float4(g.v[4 * j] - L, g.v[4 * j + 1] - L, g.v[4 * j + 2] - L,
-                            g.v[4 * j + 3] - L);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (c0 + 4 * j + q < N) frow[4 * j + q] = g.v[4 * j + q] - L;
-        }
-      }
-    }
+    if (full) g.store_logp(N, L, full + r * (int64_t)N, c0);
     if (sl == 0) {
       // L is finite or NaN (the exp-sum is >= 1 unless NaN); finite means the argmax
       // element is unmasked, NaN means index 0 was taken
@@ -438,7 +468,7 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
   }
 }
 
-template <int RL, int EPL, bool VEC>
+template <int RL, int EPL, bool VEC, int OPT>
 __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const float* logits,
                                                      int64_t lstride, const uint8_t* mask,
                                                      float clip, float temp, int mode,
@@ -455,7 +485,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
     const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
-    DecodeRow<RL, EPL, VEC> d;
+    DecodeRow<RL, EPL, VEC, OPT> d;
     d.run(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, clip, temp,
           mode, a_in, seed, offset, row, sl, grp, top_k, top_p);
     if (!valid) continue;
@@ -478,7 +508,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
 // the selected action's env transition (tsp/env.py:67-93) is applied by the same lane
 // group: mask_out = mask_in minus the action, done = nothing left (group ballot),
 // i + 1, first_node.  654 B per TSP-100 row-step.
-template <int RL, int EPL, bool VEC, int UNR = CO_DECODE_UNR>
+template <int RL, int EPL, bool VEC, int OPT, int UNR = CO_DECODE_UNR>
 __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
     int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int mode,
@@ -496,7 +526,7 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
   // UNR rows per lane group per iteration: every load of all UNR rows (logits, mask,
   // i, first_node, action, ll accumulator) is issued before any row's math
   for (int64_t base = wid * RPW * UNR; base < B; base += nwaves * RPW * UNR) {
-    DecodeRow<RL, EPL, VEC> d[UNR];
+    DecodeRow<RL, EPL, VEC, OPT> d[UNR];
     int64_t rr[UNR], ain[UNR], iv[UNR], fv[UNR];
     bool vv[UNR];
     float acc[UNR];
@@ -558,7 +588,7 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
 // Greedy decode step fused with TSPEnv._step on the GreedyRow engine (the POMO /
 // multistart-greedy hot loop); same outputs as tsp_decode_step_kernel in greedy mode.
 // The mask words are updated in registers (the selected byte cleared) and stored back.
-template <int RL, int EPL, bool VEC>
+template <int RL, int EPL, int VW, int OPT>
 __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int64_t* __restrict__ action_out,
@@ -582,9 +612,9 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
       if (!take_first) fv = first_in[r];
       if (ll_accum) acc = ll_accum[r];
     }
-    GreedyRow<RL, EPL, VEC> g;
+    GreedyRow<RL, EPL, VW> g;
     g.load(valid, N, logits + r * lstride, mask_in + r * (int64_t)N, c0);
-    const float L = g.softmax_shift(clip, temp);
+    const float L = g.template softmax_shift<OPT>(clip, temp);
     float lp;
     const int sel = g.select(L, c0, lp);
     const bool feas0 = g.allowed(0);
@@ -595,19 +625,7 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
       if ((unsigned)off < 4u) g.mw[j] &= ~(0xffu << (8 * off));
       left |= g.mw[j];
     }
-    if (valid) {
-      uint8_t* orow = mask_out + r * (int64_t)N + c0;
-#pragma unroll
-      for (int j = 0; j < EPL / 4; ++j) {
-        if (VEC) {
-          if (c0 + 4 * j < N) *reinterpret_cast<uint32_t*>(orow + 4 * j) = g.mw[j];
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (c0 + 4 * j + q < N) orow[4 * j + q] = (uint8_t)(g.mw[j] >> (8 * q));
-        }
-      }
-    }
+    if (valid) g.store_mask(N, mask_out + r * (int64_t)N, c0);
     const bool any_left = (__ballot(left != 0u) & gmask) != 0;
     if (valid && sl == 0) {
       if (L != L && !feas0) set_status(status, CO_ST_INFEASIBLE);
@@ -633,11 +651,40 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
   else if (N <= 1024) LAUNCH(64, 16, V);                     \
   else LAUNCH(64, 32, V)
 
+// the uniform clip / temperature options as the OPT template flags of the greedy kernels
+#define CO_OPT_DISPATCH(LAUNCH, KERNEL, ...)                       \
+  do {                                                             \
+    const int opt_ = (clip > 0.f ? 1 : 0) | (temp != 1.f ? 2 : 0); \
+    if (opt_ == 0) {                                               \
+      constexpr int OPT = 0;                                       \
+      LAUNCH(KERNEL, __VA_ARGS__);                                 \
+    } else if (opt_ == 1) {                                        \
+      constexpr int OPT = 1;                                       \
+      LAUNCH(KERNEL, __VA_ARGS__);                                 \
+    } else if (opt_ == 2) {                                        \
+      constexpr int OPT = 2;                                       \
+      LAUNCH(KERNEL, __VA_ARGS__);                                 \
+    } else {                                                       \
+      constexpr int OPT = 3;                                       \
+      LAUNCH(KERNEL, __VA_ARGS__);                                 \
+    }                                                              \
+  } while (0)
+
 inline unsigned decode_grid(int64_t B, int N, int unr = 1) {
   const int rl = N <= 16 ? CO_RL16 : N <= 32 ? CO_RL32 : N <= 64 ? CO_RL64
                : N <= 128 ? CO_RL128 : N <= 256 ? CO_RL256 : 64;
   const int64_t waves = ((B + unr - 1) / unr * rl + 63) / 64;
   return grid_for(waves, 4, 256 * 32);
+}
+
+// widest GreedyRow load (4 / 2 / 1 elements) the row length, stride and pointers allow
+inline int greedy_vw(int64_t N, int64_t lstride, const float* logits, const uint8_t* m_in,
+                     const uint8_t* m_out, const float* full) {
+  const uintptr_t f = reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(full);
+  const uintptr_t m = reinterpret_cast<uintptr_t>(m_in) | reinterpret_cast<uintptr_t>(m_out);
+  if (N % 4 == 0 && lstride % 4 == 0 && (f & 15) == 0 && (m & 3) == 0) return 4;
+  if (N % 2 == 0 && lstride % 2 == 0 && (f & 7) == 0 && (m & 1) == 0) return 2;
+  return 1;
 }
 
 inline bool decode_vec_ok(const float* logits, int64_t lstride, const uint8_t* mask, int64_t N) {
@@ -663,21 +710,21 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
   const bool filtered = (top_k > 0 && top_k < N) || (top_p > 0.0 && top_p < 1.0);
   if (CO_GREEDY_FAST && mode == CO_DECODE_GREEDY && !filtered) {
 #define CO_GREEDY(RL, EPL, V)                                                                  \
-  hipLaunchKernelGGL((decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V>), grid, block, 0, s, B,  \
-                     (int)N, logits, lstride, mask, clip, temp, action_out, logp_sel, full,     \
-                     status)
-    if (decode_vec_ok(logits, lstride, mask, N) && (reinterpret_cast<uintptr_t>(full) & 15) == 0) {
-      CO_ROW_DISPATCH(CO_GREEDY, true);
-    } else {
-      CO_ROW_DISPATCH(CO_GREEDY, false);
+  CO_OPT_DISPATCH(hipLaunchKernelGGL, (decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>),  \
+                  grid, block, 0, s, B, (int)N, logits, lstride, mask, clip, temp, action_out,  \
+                  logp_sel, full, status)
+    switch (greedy_vw(N, lstride, logits, mask, mask, full)) {
+      case 4: CO_ROW_DISPATCH(CO_GREEDY, 4); break;
+      case 2: CO_ROW_DISPATCH(CO_GREEDY, 2); break;
+      default: CO_ROW_DISPATCH(CO_GREEDY, 1);
     }
 #undef CO_GREEDY
     return launch_status();
   }
 #define CO_DECODE(RL, EPL, V)                                                                  \
-  hipLaunchKernelGGL((decode_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N, logits,        \
-                     lstride, mask, clip, temp, mode, action_in, action_out, logp_sel, full,   \
-                     seed, offset, status, top_k, top_p)
+  CO_OPT_DISPATCH(hipLaunchKernelGGL, (decode_kernel<RL, EPL, V, OPT>), grid, block, 0, s, B,   \
+                  (int)N, logits, lstride, mask, clip, temp, mode, action_in, action_out,      \
+                  logp_sel, full, seed, offset, status, top_k, top_p)
   if (decode_vec_ok(logits, lstride, mask, N)) {
     CO_ROW_DISPATCH(CO_DECODE, true);
   } else {
@@ -715,25 +762,25 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
   if (CO_GREEDY_FAST && mode == CO_DECODE_GREEDY) {
     const dim3 grid(decode_grid(B, (int)N)), block(256);
 #define CO_TDG(RL, EPL, V)                                                                     \
-  hipLaunchKernelGGL((tsp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V>), grid, block, 0, s, \
-                     B, (int)N, logits, lstride, mask_in, clip, temp, action_out, logp_sel,     \
-                     mask_out, i_in, i_out, first_in, first_out, first_mode, done, step_reward, \
-                     ll_accum, status)
-    if (decode_vec_ok(logits, lstride, mask_in, N) &&
-        (reinterpret_cast<uintptr_t>(mask_out) & 3) == 0) {
-      CO_ROW_DISPATCH(CO_TDG, true);
-    } else {
-      CO_ROW_DISPATCH(CO_TDG, false);
+  CO_OPT_DISPATCH(hipLaunchKernelGGL,                                                          \
+                  (tsp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), grid, block, 0, \
+                  s, B, (int)N, logits, lstride, mask_in, clip, temp, action_out, logp_sel,     \
+                  mask_out, i_in, i_out, first_in, first_out, first_mode, done, step_reward,    \
+                  ll_accum, status)
+    switch (greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr)) {
+      case 4: CO_ROW_DISPATCH(CO_TDG, 4); break;
+      case 2: CO_ROW_DISPATCH(CO_TDG, 2); break;
+      default: CO_ROW_DISPATCH(CO_TDG, 1);
     }
 #undef CO_TDG
     return launch_status();
   }
   const dim3 grid(decode_grid(B, (int)N, CO_DECODE_UNR)), block(256);
 #define CO_TDS(RL, EPL, V)                                                                     \
-  hipLaunchKernelGGL((tsp_decode_step_kernel<RL, EPL, V>), grid, block, 0, s, B, (int)N,       \
-                     logits, lstride, mask_in, clip, temp, mode, action_in, action_out,        \
-                     logp_sel, seed, offset, mask_out, i_in, i_out, first_in, first_out,       \
-                     first_mode, done, step_reward, ll_accum, status)
+  CO_OPT_DISPATCH(hipLaunchKernelGGL, (tsp_decode_step_kernel<RL, EPL, V, OPT>), grid, block,   \
+                  0, s, B, (int)N, logits, lstride, mask_in, clip, temp, mode, action_in,       \
+                  action_out, logp_sel, seed, offset, mask_out, i_in, i_out, first_in,         \
+                  first_out, first_mode, done, step_reward, ll_accum, status)
   if (decode_vec_ok(logits, lstride, mask_in, N) &&
       (reinterpret_cast<uintptr_t>(mask_out) & 3) == 0) {
     CO_ROW_DISPATCH(CO_TDS, true);

@@ -54,7 +54,7 @@ def _rand_mask(b, n, g):
     return m
 
 
-@pytest.mark.parametrize("n", [20, 64, 100, 129, 500])
+@pytest.mark.parametrize("n", [20, 50, 64, 100, 129, 500])
 @pytest.mark.parametrize("clip", [0.0, 10.0])
 def test_decode_greedy_and_evaluate(dev, n, clip):
     g = torch.Generator().manual_seed(n)
