@@ -289,13 +289,32 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
   if (STATE) copy_tile_out(smem, rows * N, mask_out + row0 * N);
 }
 
+// ascending sort of EPL u64 keys in registers (Batcher odd-even merge network)
+template <int EPL>
+__device__ __forceinline__ void sort_keys(uint64_t (&k)[EPL]) {
+  static_assert((EPL & (EPL - 1)) == 0, "EPL must be a power of two");
+#pragma unroll
+  for (int p = 1; p < EPL; p <<= 1)
+#pragma unroll
+    for (int q = p; q > 0; q >>= 1)
+#pragma unroll
+      for (int j = q % p; j + q < EPL; j += 2 * q)
+#pragma unroll
+        for (int i = 0; i < q; ++i)
+          if (i + j + q < EPL && (i + j) / (2 * p) == (i + j + q) / (2 * p)) {
+            const uint64_t a = k[i + j], b = k[i + j + q];
+            k[i + j] = a < b ? a : b;
+            k[i + j + q] = a < b ? b : a;
+          }
+}
 
 // ----------------------------------------------------------------------------- SLAP
 // SLAP episode (slap/env.py:38-143), G lanes per instance, 256/G instances per
 // workgroup.  Lane `sl` keeps locations c = sl + G*k (k < EPL): their depot distance
 // and a free bit in VGPRs.  Step t assigns product t (to_choose after reset is
-// 0..P-1) to the step's location: the closest-free policy is a DPP argmin over the
-// group (ties -> lowest index, torch.argmin on depot_loc_dist masked to inf), a
+// 0..P-1) to the step's location: the closest-free policy is a DPP min over the
+// lanes' sorted candidate heads (ties -> lowest index, torch.argmin on depot_loc_dist
+// masked to inf), a
 // teacher action is one broadcast load of the step-major action row; python's
 // negative-index wrap applies to the mask write and the reward's location lookup
 // (the int32 assignment keeps the raw value, slap/env.py:50-62).  The reward then runs
@@ -348,24 +367,37 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
     xr[k] = c < L ? lrow[c] : make_float2(0.f, 0.f);
     pr[k] = c < O * K ? prow[c] : 0;
   }
+  // closest-free = the free locations in increasing (distance, index) order.  Each lane
+  // sorts its EPL candidates once (keys: order-preserving u32 of the distance, then the
+  // location); a step is then a group min over the lanes' heads and a pop by the owner,
+  // instead of an EPL-wide scan + argmin and a slot clear.  A distance that is not below
+  // +inf (taken, depot, pad, NaN) is never chosen; with no candidate left the action is 0.
+  uint64_t key[EPL];
+  if (CLOSEST) {
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const uint32_t u = __float_as_uint(dd[k]);
+      const uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+      key[k] = ((uint64_t)ord << 32) | (uint32_t)(sl + G * k);
+    }
+    sort_keys<EPL>(key);
+  }
+  constexpr uint32_t kOrdInf = 0xff800000u;  // ordered key of +inf
   bool range = false;
   for (int t = 0; t < P; ++t) {
     int64_t a64;
     if (CLOSEST) {
-      float best = __builtin_inff();
-      int bi = 0x7fffffff;
+      const uint32_t hh = (uint32_t)(key[0] >> 32);
+      const uint32_t gm = grp_reduce<G>(hh, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+      const uint32_t cand = hh == gm ? (uint32_t)key[0] : 0xffffffffu;
+      const uint32_t gi =
+          grp_reduce<G>(cand, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+      const bool any = gm < kOrdInf;
+      a64 = any ? (int64_t)gi : 0;
+      if (any && sl == (int)(gi % G)) {  // the owner's head is the chosen location
 #pragma unroll
-      for (int k = 0; k < EPL; ++k)
-        if (dd[k] < best) {
-          best = dd[k];
-          bi = sl + G * k;
-        }
-      grp_argmin_split<G>(best, bi);
-      a64 = bi == 0x7fffffff ? 0 : bi;
-      if (bi != 0x7fffffff && sl == bi % G) {
-        const int slot = bi / G;
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) dd[k] = k == slot ? __builtin_inff() : dd[k];
+        for (int k = 0; k < EPL - 1; ++k) key[k] = key[k + 1];
+        key[EPL - 1] = ~0ull;
       }
       if (live && sl == 0) acts_out[(int64_t)t * B + bb] = a64;
     } else {
