@@ -94,12 +94,15 @@ int co_cvrp_reset(int64_t batch, int64_t num_loc, const float* depot, const floa
 /* CVRPEnv._step fused with get_action_mask (cvrp/env.py:73-105,137-149):
  *   d = demand[b, clamp(a-1, 0, N-1)]; used_out = (used_in + d) * (a != 0)
  *   visited_out = visited_in with [a] = 1 (in-place allowed); current_out = a
- *   done = sum(visited_out) == N+1 ; reward = 0 (bool); action_mask recomputed. */
+ *   done = sum(visited_out) == N+1 ; reward = 0 (bool); action_mask recomputed.
+ * not_done (optional) is atomically incremented by the number of rows not done
+ * (the `while not td["done"].all()` poll of constructive/base.py:245 without a second
+ * pass over `done`); the caller zeroes it. */
 int co_cvrp_step(int64_t batch, int64_t num_loc, const int64_t* action, const float* demand,
                  const float* used_in, float* used_out, const float* vehicle_capacity,
                  const uint8_t* visited_in, uint8_t* visited_out, int64_t* current_out,
                  uint8_t* done, uint8_t* reward, uint8_t* action_mask, int32_t* status,
-                 void* stream);
+                 int32_t* not_done, void* stream);
 
 /* CVRPEnv.get_action_mask alone (cvrp/env.py:137-149). current_node is [B,1]. */
 int co_cvrp_action_mask(int64_t batch, int64_t num_loc, const float* demand, const float* used,

@@ -2,12 +2,13 @@
 // stand-alone mask, episode reward with the validity/capacity check, and the
 // nearest-feasible bench policy.
 //
-// Step layout: one wavefront per instance (grid-stride), lanes over the N+1
-// columns: visited update, capacity test `demand + used > capacity` (strict, f32,
-// no contraction), visited-sum and any-feasible-customer are wave reductions
-// (ballot / shuffle).  The capacity arithmetic follows cvrp/env.py:83-85 exactly:
-// used = (used + d) * float(a != 0).
+// Step layout: 16-B-aligned buffers take the row-tile kernel (cvrp_step_tile_kernel,
+// below); otherwise one wavefront per instance (grid-stride), lanes over the N+1
+// columns.  Capacity test `demand + used > capacity` (strict, f32, no contraction);
+// visited-sum and any-feasible-customer are row reductions.  The capacity arithmetic
+// follows cvrp/env.py:83-85 exactly: used = (used + d) * float(a != 0).
 #include "co_common.hpp"
+#include "co_tile.hpp"
 
 using namespace co;
 
@@ -76,9 +77,11 @@ __global__ __launch_bounds__(256) void cvrp_reset_kernel(int64_t B, int N, const
 __global__ __launch_bounds__(256) void cvrp_step_kernel(
     int64_t B, int N, const int64_t* action, const float* demand, const float* used_in,
     float* used_out, const float* vcap, const uint8_t* vis_in, uint8_t* vis_out, int64_t* cur_out,
-    uint8_t* done, uint8_t* reward, uint8_t* mask, int32_t* status) {
+    uint8_t* done, uint8_t* reward, uint8_t* mask, int32_t* status,
+    int32_t* not_done) {
   const int lane = lane_id();
   const int64_t wpb = blockDim.x >> 6;
+  int left = 0;
   for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
        b += (int64_t)gridDim.x * wpb) {
     const int64_t a = action[b];
@@ -96,8 +99,241 @@ __global__ __launch_bounds__(256) void cvrp_step_kernel(
       used_out[b] = u;
       if (cur_out) cur_out[b] = a;
       done[b] = vsum == N + 1;
+      left += vsum != N + 1;
       reward[b] = 0;
     }
+  }
+  if (not_done && lane == 0 && left) atomicAdd(not_done, left);
+}
+
+// ---------------------------------------------------------------------------
+// Tile step: one 256-thread workgroup owns R consecutive rows (R a multiple of 16, so
+// the [R, N+1] byte tiles of visited / action_mask start 16-B aligned).  The visited
+// tile streams through registers in 16-B chunks (at most kCvrpCpt per thread, kept in
+// registers across the barrier), the [R, N] demand tile is staged in LDS by float4
+// loads, and the two row reductions of the step (visited sum for `done`, "any feasible
+// customer" for the depot column) are per-chunk partials in LDS summed per row.  The
+// depot byte of each row is patched into its chunk after the barrier, so every byte of
+// the mask tile is written once by a 16-B store.  `not_done` (optional) receives one
+// atomicAdd per workgroup: the number of its rows that are not done.
+constexpr int kCvrpCpt = 2;
+constexpr int kCvrpMaxRows = 64;
+
+template <int THREADS>
+__global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
+    int64_t B, int N, int R, const int64_t* __restrict__ action, const float* __restrict__ demand,
+    const float* __restrict__ used_in, float* __restrict__ used_out,
+    const float* __restrict__ vcap, const uint8_t* vis_in, uint8_t* vis_out,
+    int64_t* __restrict__ cur_out, uint8_t* __restrict__ done, uint8_t* __restrict__ reward,
+    uint8_t* __restrict__ mask, int32_t* status, int32_t* not_done) {
+  extern __shared__ float s_dem[];  // [R, N]
+  __shared__ int s_act[kCvrpMaxRows];
+  __shared__ float s_u[kCvrpMaxRows], s_cap[kCvrpMaxRows];
+  __shared__ int s_cnt[kCvrpMaxRows], s_feas[kCvrpMaxRows];
+  __shared__ int s_part[2 * kCvrpCpt * THREADS];  // per chunk: (sum, any) of its <= 2 rows
+  const int tid = threadIdx.x;
+  const int NC = N + 1;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int rows = (int)((B - row0) < R ? (B - row0) : R);
+  const int nbytes = rows * NC;
+  const int nchunks = (nbytes + 15) >> 4;
+  const uint8_t* vsrc = vis_in + row0 * NC;
+
+  // every global load of the tile is issued before the first barrier
+  int64_t a_raw = 0;
+  float uin = 0.f, cap = 0.f;
+  if (tid < rows) {
+    a_raw = action[row0 + tid];
+    uin = used_in[row0 + tid];
+    cap = vcap[row0 + tid];
+  }
+  uint4 v[kCvrpCpt];
+#pragma unroll
+  for (int k = 0; k < kCvrpCpt; ++k) {
+    const int c = tid + k * THREADS;
+    if (c < nchunks) v[k] = tile_load(vsrc, c << 4, nbytes, true);
+  }
+  // demand tile -> LDS by LDS-DMA; the helper's vmcnt(0) + barrier also covers the loads above
+  stage_bytes_lds(reinterpret_cast<const unsigned char*>(demand + row0 * N), rows * N * 4,
+                  reinterpret_cast<unsigned char*>(s_dem));
+  if (tid < rows) {  // cvrp/env.py:79-85
+    const bool bad = a_raw < 0 || a_raw > N;
+    if (bad) set_status(status, CO_ST_INDEX_RANGE);
+    s_act[tid] = bad ? -1 : (int)a_raw;
+    s_cap[tid] = cap;
+    int64_t di = a_raw - 1;
+    di = di < 0 ? 0 : (di > N - 1 ? N - 1 : di);
+    s_u[tid] = (uin + s_dem[tid * N + di]) * ((a_raw != 0) ? 1.0f : 0.0f);
+  }
+  __syncthreads();
+
+  // Each chunk spans at most two rows (NC >= 17): r0 from byte 0, r1 from byte `split`.
+  // Per byte only selects (no branches); each chunk leaves (sum, any-feasible) of both row
+  // parts in LDS and one thread per row adds its ~NC/16 parts after the barrier.
+  uint4 m[kCvrpCpt];
+  uint8_t* vdst = vis_out + row0 * NC;
+#pragma unroll
+  for (int k = 0; k < kCvrpCpt; ++k) {
+    const int ch = tid + k * THREADS;
+    if (ch >= nchunks) continue;
+    const int off = ch << 4;
+    const int r0 = off / NC, c0 = off - r0 * NC;
+    const int split = NC - c0;  // bytes of row r0 in this chunk
+    const int r1 = r0 + 1;
+    const bool has1 = split < 16 && r1 < rows;
+    const int act0 = s_act[r0], act1 = has1 ? s_act[r1] : -1;
+    const float u0 = s_u[r0], cp0 = s_cap[r0];
+    const float u1 = has1 ? s_u[r1] : 0.f, cp1 = has1 ? s_cap[r1] : 0.f;
+    const int dbase = off - r0 - 1;  // s_dem index of byte j: dbase + j (row r0), one less (r1)
+    union {
+      uint4 v;
+      uint8_t b[16];
+    } uv, um;
+    uv.v = v[k];
+    // all 16 demand reads issued before any use (a short-circuit `||` would put each
+    // behind a branch and an lgkmcnt(0) wait)
+    float dm[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      int di = dbase + j - (j >= split ? 1 : 0);
+      dm[j] = s_dem[di < 0 ? 0 : di];
+    }
+    int cnt0 = 0, cnt1 = 0, feas0 = 0, feas1 = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const bool sec = j >= split;
+      const int c = sec ? j - split : c0 + j;
+      uint8_t x = uv.b[j];
+      x = (c == (sec ? act1 : act0)) ? (uint8_t)1 : x;
+      uv.b[j] = x;
+      const bool masked = (x != 0) | (dm[j] + (sec ? u1 : u0) > (sec ? cp1 : cp0));
+      const int mk = (c > 0 && off + j < nbytes && !masked) ? 1 : 0;
+      um.b[j] = (uint8_t)mk;
+      cnt0 += sec ? 0 : x;
+      cnt1 += sec ? x : 0;
+      feas0 |= sec ? 0 : mk;
+      feas1 |= sec ? mk : 0;
+    }
+    s_part[2 * ch] = cnt0 | (feas0 << 16);
+    s_part[2 * ch + 1] = cnt1 | (feas1 << 16);
+    tile_store(vdst, off, nbytes, true, uv.v);
+    m[k] = um.v;
+  }
+  __syncthreads();
+  if (tid < rows) {  // row sums over the row's chunk parts
+    int cnt = 0, feas = 0;
+    const int ch_lo = (tid * NC) >> 4, ch_hi = ((tid + 1) * NC - 1) >> 4;
+    for (int ch = ch_lo; ch <= ch_hi; ++ch) {
+      const int pv = s_part[2 * ch + (((ch << 4) / NC) == tid ? 0 : 1)];
+      cnt += pv & 0xffff;
+      feas |= pv >> 16;
+    }
+    s_cnt[tid] = cnt;
+    s_feas[tid] = feas;
+  }
+  __syncthreads();
+  // depot column of the rows starting in each chunk (cvrp/env.py:146-148), patched with
+  // static byte positions only (a dynamic byte index would spill the chunk to scratch)
+  uint8_t* mdst = mask + row0 * NC;
+#pragma unroll
+  for (int k = 0; k < kCvrpCpt; ++k) {
+    const int ch = tid + k * THREADS;
+    if (ch >= nchunks) continue;
+    const int off = ch << 4;
+    const int r0 = off / NC, c0 = off - r0 * NC;
+    const int split = NC - c0;
+    const int r1 = r0 + 1;
+    const int pos0 = c0 == 0 ? 0 : -1;
+    const int pos1 = (split < 16 && r1 < rows) ? split : -1;
+    const uint32_t d0 = !((s_act[r0] == 0) && s_feas[r0]);
+    const uint32_t d1 = pos1 >= 0 ? (uint32_t) !((s_act[r1] == 0) && s_feas[r1]) : 0u;
+    uint32_t w[4] = {m[k].x, m[k].y, m[k].z, m[k].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = q * 4 + e;
+        const uint32_t keep = ~(0xffu << (8 * e));
+        if (j == pos0) w[q] = (w[q] & keep) | (d0 << (8 * e));
+        if (j == pos1) w[q] = (w[q] & keep) | (d1 << (8 * e));
+      }
+    }
+    tile_store(mdst, off, nbytes, true, make_uint4(w[0], w[1], w[2], w[3]));
+  }
+  if (tid < rows) {
+    const int64_t b = row0 + tid;
+    used_out[b] = s_u[tid];
+    if (cur_out) cur_out[b] = a_raw;
+    const bool dn = s_cnt[tid] == NC;
+    done[b] = dn;
+    reward[b] = 0;
+    if (not_done) {
+      const int left = __popcll(__ballot(!dn));
+      if (tid == 0 && left) atomicAdd(not_done, left);
+    }
+  }
+}
+
+// Nearest-feasible policy, G lanes per instance: node c = 1 + sl + k*G (coalesced float2
+// and mask-byte loads across the group, all KM of a lane issued before any use),
+// Euclidean distance as torch (f32, no contraction), group argmin with the lowest index
+// on ties, depot when no customer is feasible.  KM = 0: runtime loop for large N.  Loop
+// counts are wave-uniform (the DPP reductions need every lane).
+template <int G, int KM>
+__global__ __launch_bounds__(256) void cvrp_nearest_group_kernel(int64_t B, int N,
+                                                                 const float2* __restrict__ locs,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 const int64_t* __restrict__ cur,
+                                                                 int64_t* __restrict__ out) {
+  const int lane = lane_id(), sl = lane % G;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int K = (N + G - 1) / G;
+  for (int64_t base = wid * (64 / G); base < B; base += nwaves * (64 / G)) {
+    const int64_t b = base + lane / G;
+    const bool valid = b < B;
+    const int64_t r = valid ? b : 0;
+    const float2* lrow = locs + r * (int64_t)(N + 1);
+    const uint8_t* mrow = mask + r * (int64_t)(N + 1);
+    int64_t c0 = cur[r];
+    float best = __builtin_inff();
+    int bi = 0x7fffffff;
+    if (KM > 0) {
+      // unconditional loads at clamped columns and select-based updates: a predicated
+      // load would be sunk by the compiler behind the mask test and its vmcnt(0) wait
+      float2 q[KM > 0 ? KM : 1];
+      uint8_t mk[KM > 0 ? KM : 1];
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int c = 1 + sl + k * G;
+        const int cc = c <= N ? c : N;
+        mk[k] = mrow[cc];
+        q[k] = lrow[cc];
+      }
+      c0 = (c0 < 0 || c0 > N) ? 0 : c0;
+      const float2 p = lrow[c0];
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int c = 1 + sl + k * G;
+        const float d = edge_len(p.x, p.y, q[k].x, q[k].y);
+        const bool take = (k < K) & (c <= N) & (mk[k] != 0) & (d < best);
+        best = take ? d : best;
+        bi = take ? c : bi;
+      }
+    } else {
+      c0 = (c0 < 0 || c0 > N) ? 0 : c0;
+      const float2 p = lrow[c0];
+      for (int k = 0; k < K; ++k) {
+        const int c = 1 + sl + k * G;
+        if (valid && c <= N && mrow[c]) {
+          const float2 q = lrow[c];
+          const float d = edge_len(p.x, p.y, q.x, q.y);
+          if (d < best) { best = d; bi = c; }
+        }
+      }
+    }
+    grp_argmin_split<G>(best, bi);
+    if (valid && sl == 0) out[b] = bi == 0x7fffffff ? 0 : bi;
   }
 }
 
@@ -188,35 +424,6 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void cvrp_nearest_kernel(int64_t B, int N, const float2* locs,
-                                                           const uint8_t* mask,
-                                                           const int64_t* cur, int64_t* out) {
-  const int lane = lane_id();
-  const int64_t wpb = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
-       b += (int64_t)gridDim.x * wpb) {
-    const float2* lrow = locs + b * (int64_t)(N + 1);
-    const uint8_t* mrow = mask + b * (int64_t)(N + 1);
-    int64_t c0 = cur[b];
-    c0 = (c0 < 0 || c0 > N) ? 0 : c0;
-    const float2 p = lrow[c0];
-    float best = __builtin_inff();
-    int bi = 0x7fffffff;
-    bool any = false;
-    for (int c = lane + 1; c <= N; c += 64) {
-      if (mrow[c]) {
-        any = true;
-        const float2 q = lrow[c];
-        const float d = edge_len(p.x, p.y, q.x, q.y);
-        if (d < best || (d == best && c < bi)) { best = d; bi = c; }
-      }
-    }
-    wave_argmin(best, bi);
-    const bool anyf = __any(any);
-    if (lane == 0) out[b] = anyf ? bi : 0;
-  }
-}
-
 }  // namespace
 
 extern "C" int co_cvrp_reset(int64_t B, int64_t N, const float* depot, const float* locs_in,
@@ -242,15 +449,31 @@ extern "C" int co_cvrp_step(int64_t B, int64_t N, const int64_t* action, const f
                             const float* used_in, float* used_out, const float* vcap,
                             const uint8_t* vis_in, uint8_t* vis_out, int64_t* cur_out,
                             uint8_t* done, uint8_t* reward, uint8_t* mask, int32_t* status,
-                            void* stream) {
+                            int32_t* not_done, void* stream) {
   if (B < 0 || N <= 0) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!action || !demand || !used_in || !used_out || !vcap || !vis_in || !vis_out || !done ||
       !reward || !mask)
     return CO_E_INVAL;
+  // 256-thread tiles of R = min(64, 8192 / (N+1)) & ~15 rows (single-wave 16-row tiles
+  // measured slower at N = 100: 16.3 vs 12.2 us per step at B = 32,768)
+  const int64_t NC = N + 1;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(vis_in) | reinterpret_cast<uintptr_t>(vis_out) |
+                         reinterpret_cast<uintptr_t>(mask) | reinterpret_cast<uintptr_t>(demand)) &
+                        15) == 0;
+  int R = (int)((256 * kCvrpCpt * 16) / NC);
+  R = (R > kCvrpMaxRows ? kCvrpMaxRows : R) & ~15;
+  if (N >= 16 && aligned && R >= 16 && (size_t)R * N * sizeof(float) <= 64 * 1024) {
+    const unsigned grid = (unsigned)((B + R - 1) / R);
+    hipLaunchKernelGGL(cvrp_step_tile_kernel<256>, dim3(grid), dim3(256),
+                       (size_t)R * N * sizeof(float), (hipStream_t)stream, B, (int)N, R, action,
+                       demand, used_in, used_out, vcap, vis_in, vis_out, cur_out, done, reward,
+                       mask, status, not_done);
+    return launch_status();
+  }
   hipLaunchKernelGGL(cvrp_step_kernel, dim3(grid_for(B, 4, 256 * 32)), dim3(256), 0,
                      (hipStream_t)stream, B, (int)N, action, demand, used_in, used_out, vcap,
-                     vis_in, vis_out, cur_out, done, reward, mask, status);
+                     vis_in, vis_out, cur_out, done, reward, mask, status, not_done);
   return launch_status();
 }
 
@@ -306,8 +529,17 @@ extern "C" int co_cvrp_nearest_action(int64_t B, int64_t N, const float* locs,
   if (B < 0 || N <= 0) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!locs || !mask || !cur || !out) return CO_E_INVAL;
-  hipLaunchKernelGGL(cvrp_nearest_kernel, dim3(grid_for(B, 4, 256 * 32)), dim3(256), 0,
-                     (hipStream_t)stream, B, (int)N, reinterpret_cast<const float2*>(locs), mask,
-                     cur, out);
+  if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  const float2* l2 = reinterpret_cast<const float2*>(locs);
+  const hipStream_t s = (hipStream_t)stream;
+#define CO_CNG(GG, KK)                                                                  \
+  hipLaunchKernelGGL((cvrp_nearest_group_kernel<GG, KK>),                             \
+                     dim3(grid_for(B, 4 * (64 / GG), 256 * 32)), dim3(256), 0, s, B, (int)N, l2, \
+                     mask, cur, out)
+  if (N <= 64) CO_CNG(8, 8);
+  else if (N <= 160) CO_CNG(16, 10);
+  else if (N <= 320) CO_CNG(32, 10);
+  else CO_CNG(64, 0);
+#undef CO_CNG
   return launch_status();
 }

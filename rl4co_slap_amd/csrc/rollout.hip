@@ -15,31 +15,11 @@ using namespace co;
 
 namespace {
 
-typedef __attribute__((address_space(3))) void lds_void;
 
 // NW template value the launchers pick for N (1, 2 or 4 words of 64 bits)
 inline int NW_launch(int64_t n) {
   const int w = (int)((n + 63) / 64);
   return w <= 1 ? 1 : (w == 2 ? 2 : 4);
-}
-
-// Copy `nbytes` contiguous bytes global -> LDS with LDS-DMA (global_load_lds_dwordx4):
-// every wave-instruction moves 1 KiB to a wave-uniform LDS base + lane*16, no VGPR
-// round trip, all pieces in flight before the single wait.  `src` and `dst` must be
-// 16-byte aligned; a tail of < 16 bytes is copied with plain loads.  Ends with the
-// vmcnt drain + workgroup barrier that make the tile visible.
-__device__ __forceinline__ void stage_bytes_lds(const unsigned char* __restrict__ src, int nbytes,
-                                                unsigned char* dst) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int n16 = nbytes & ~15;
-  for (int base = wave * 1024; base < n16; base += nw * 1024) {
-    const int off = base + lane * 16;
-    if (off < n16)
-      __builtin_amdgcn_global_load_lds((const void*)(src + off), (lds_void*)(dst + base), 16, 0, 0);
-  }
-  for (int k = n16 + (int)threadIdx.x; k < nbytes; k += blockDim.x) dst[k] = src[k];
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
 }
 
 // Columns [c_lo, c_hi) of a row of visited bits -> mask bytes (1 = still feasible) of

@@ -109,7 +109,7 @@ class CVRPEnv(RL4COEnvBase):
         mask = torch.empty((b, n + 1), dtype=torch.bool, device=dev)
         nat.call("co_cvrp_step", b, n, nat.ptr(action), nat.ptr(demand), nat.ptr(used),
                  nat.ptr(used_out), nat.ptr(vcap), nat.ptr(visited), nat.ptr(visited_out),
-                 nat.ptr(cur), nat.ptr(done), nat.ptr(reward), nat.ptr(mask), None,
+                 nat.ptr(cur), nat.ptr(done), nat.ptr(reward), nat.ptr(mask), None, None,
                  nat.stream_of(demand))
         td.update({"current_node": cur, "used_capacity": used_out, "visited": visited_out,
                    "reward": reward, "done": done, "action_mask": mask})

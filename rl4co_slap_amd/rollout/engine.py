@@ -306,8 +306,9 @@ class CVRPStepwiseEpisode:
     """Reference-shaped CVRP loop: one ``co_cvrp_nearest_action`` + ``co_cvrp_step``
     launch pair per env step with the TensorDict state in HBM, ``while not
     done.all()`` replaced by graph chunks and a device-side not-done count per step
-    (``co_count_not_done``) read once per chunk.  No instance can finish before N
-    steps, so steps 0..N-1 are one graph; later chunks are ``chunk`` steps.  Per-step
+    (accumulated by ``co_cvrp_step`` itself) read once per chunk.  No instance can be done
+    before step N (N customers and one depot visit), so steps 0..N-1 are one graph that
+    counts nothing; later chunks are ``chunk`` steps.  Per-step
     ``current_node``/``used_capacity`` rows are kept, so the state at the exact
     all-done step T is returned even when the last chunk runs past it (steps after T
     only repeat the depot action)."""
@@ -341,6 +342,7 @@ class CVRPStepwiseEpisode:
         self.T = None
 
     def _reset(self, s):
+        self.not_done.zero_()  # per-step counters, incremented by co_cvrp_step
         nat.call("co_cvrp_reset", self.b, self.n, nat.ptr(self.depot), nat.ptr(self.locs_in),
                  nat.ptr(self.demand), self.vcap, nat.ptr(self.locs), nat.ptr(self.cur[0]),
                  nat.ptr(self.used[0]), nat.ptr(self.vcap_t), nat.ptr(self.visited[0]),
@@ -354,8 +356,7 @@ class CVRPStepwiseEpisode:
                  nat.ptr(self.used[t]), nat.ptr(self.used[t + 1]), nat.ptr(self.vcap_t),
                  nat.ptr(self.visited[k]), nat.ptr(self.visited[k1]), nat.ptr(self.cur[t + 1]),
                  nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.mask[k1]),
-                 nat.ptr(self.status), s)
-        nat.call("co_count_not_done", nat.ptr(self.done), self.b, nat.ptr(self.not_done[t:]), s)
+                 nat.ptr(self.status), nat.ptr(self.not_done[t:]) if t >= self.n else None, s)
 
     def _ranges(self):
         first = min(self.n, self.max_steps)
@@ -391,7 +392,7 @@ class CVRPStepwiseEpisode:
         self.T = None
         for t0, t1, g in self.graphs:
             g.replay()
-            if t1 >= self.n and int(self.not_done[t1 - 1].item()) == 0:
+            if t1 > self.n and int(self.not_done[t1 - 1].item()) == 0:
                 nd = self.not_done[t0:t1].cpu()
                 self.T = t0 + int((nd == 0).nonzero()[0, 0]) + 1
                 break

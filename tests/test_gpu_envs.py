@@ -141,6 +141,68 @@ def test_cvrp_random_feasible_episode(dev, b, n):
     assert_reward_close(env.get_reward(td, acts.to(dev)), ref_env.get_reward(td_ref, acts))
 
 
+def _cvrp_step_raw(td, action, offset=0, not_done=None):
+    """co_cvrp_step on copies of the state; `offset` bytes shift the visited / mask
+    buffers off 16-B alignment (the per-instance fallback kernel)."""
+    from rl4co_slap_amd import _native as nat
+
+    b, n = td["demand"].shape
+    dev = td["demand"].device
+
+    def shifted(x):
+        flat = torch.empty(x.numel() + 16, dtype=torch.uint8, device=dev)
+        v = flat[offset:offset + x.numel()].view(x.shape)
+        v.copy_(x.view(torch.uint8) if x.dtype == torch.bool else x)
+        return v
+
+    vis_in = shifted(td["visited"])
+    vis_out, mask = shifted(td["visited"]), shifted(td["action_mask"])
+    used_out = torch.empty_like(td["used_capacity"])
+    cur = torch.empty((b, 1), dtype=torch.int64, device=dev)
+    done = torch.empty(b, dtype=torch.bool, device=dev)
+    rew = torch.empty(b, dtype=torch.bool, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    nat.call("co_cvrp_step", b, n, nat.ptr(action), nat.ptr(td["demand"]),
+             nat.ptr(td["used_capacity"]), nat.ptr(used_out), nat.ptr(td["vehicle_capacity"]),
+             nat.ptr(vis_in), nat.ptr(vis_out), nat.ptr(cur), nat.ptr(done), nat.ptr(rew),
+             nat.ptr(mask), nat.ptr(status),
+             nat.ptr(not_done) if not_done is not None else None, nat.stream_of(action))
+    return {"visited": vis_out, "action_mask": mask.view(torch.bool), "used_capacity": used_out,
+            "current_node": cur, "done": done, "reward": rew, "status": status}
+
+
+# tile rows R = min(64, 8192 // (N+1)) & ~15: N=100 -> 64, N=200 -> 32, N=511 -> 16;
+# N=600, N < 16 and misaligned buffers take the per-instance kernel
+@pytest.mark.parametrize("b,n,offset", [(70, 100, 0), (70, 100, 3), (41, 200, 0), (19, 511, 0),
+                                        (9, 600, 0), (64, 15, 0)])
+def test_cvrp_step_tile_paths_and_not_done(dev, b, n, offset):
+    ref_env, td_ref, env, td = _cvrp_pair(b, n, 4242 + n, dev)
+    g = torch.Generator().manual_seed(5)
+    t = 0
+    while not td_ref["done"].all():
+        a = torch.multinomial(td_ref["action_mask"].float(), 1, generator=g).squeeze(-1)
+        td_ref["action"] = a
+        td_ref = ref_env.step(td_ref)["next"]
+        nd = torch.zeros(1, dtype=torch.int32, device=dev)
+        out = _cvrp_step_raw(td, a.to(dev), offset, nd)
+        for k in ("visited", "action_mask", "used_capacity", "current_node", "done", "reward"):
+            assert_same(out[k], td_ref[k], f"{k}@{t}")
+        assert int(nd.item()) == int((~td_ref["done"]).sum()), t
+        assert int(out["status"].item()) == 0
+        td["action"] = a.to(dev)
+        td = env.step(td)["next"]
+        t += 1
+
+
+def test_cvrp_step_out_of_range_action_flag(dev):
+    _, _, env, td = _cvrp_pair(64, 30, 3, dev)
+    a = torch.zeros(64, dtype=torch.int64, device=dev)
+    a[5] = 31
+    out = _cvrp_step_raw(td, a)
+    assert int(out["status"].item()) & 8  # CO_ST_INDEX_RANGE
+    assert int(out["visited"][5].sum().item()) == 0  # no visited update for the bad row
+
+
 def test_cvrp_nearest_policy_and_mask(dev):
     from rl4co_slap_amd import _native as nat
 

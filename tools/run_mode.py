@@ -1,0 +1,50 @@
+"""Run one bench.py mode alone (for rocprofv3 kernel traces of a single path).
+
+    python tools/run_mode.py cvrp|slap|slap65k|pomo|tsp [--k K]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode")
+    ap.add_argument("--k", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    from rl4co_slap_amd import _native
+
+    _native.load()
+    if a.mode == "cvrp":
+        out = bench.bench_cvrp(32768, 100, a.k, 1, 0, dev)
+    elif a.mode == "slap":
+        out = bench.bench_slap(16384, a.k, 1, 0, dev)
+    elif a.mode == "slap65k":
+        out = bench.bench_slap(65536, a.k, 1, 0, dev, stepwise=False)
+    elif a.mode == "pomo":
+        out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev)
+    elif a.mode == "tsp":
+        from rl4co_slap_amd.rollout.engine import TSPFusedEpisode
+
+        locs, acts = bench.tsp_inputs(65536, 100, 0)
+        ep = TSPFusedEpisode(locs.to(dev), acts.to(dev), policy="teacher", check=True)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        wall, ev = bench.timed(lambda: ep._launch(sh), a.k, 2, 1, dev)
+        out = {"launch_us": ev / a.k * 1e6, "wall_us": wall / a.k * 1e6}
+    else:
+        raise SystemExit(f"unknown mode {a.mode}")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
