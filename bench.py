@@ -306,6 +306,8 @@ def annotate_modes(modes, n, world):
         "tsp_fused_nearest": lambda m: (17 * n + 30) / n,
         "slap_fused_closest": lambda m: 2754 / 20,
         "slap_fused_closest_b65536": lambda m: 2754 / 20,
+        "slap_fused_random": lambda m: 2354 / 20,
+        "slap_fused_random_b65536": lambda m: 2354 / 20,
         "slap_stepwise_graph": lambda m: 234 + 1684 / 20,
         "pomo_tsp100": lambda m: 6 * n + 54,
         "cvrp_fused_nearest": lambda m: (8 + 12 * n + 8 * m["episode_steps"] + 10 * (n + 1) + 25)
@@ -346,6 +348,20 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
                                  "bytes_per_episode": 2754,
                                  "achieved_GBps": b * 2754 / (ev / (4 * k)) / 1e9}
     del fu
+    # random-feasible policy, teacher-forced like the TSP headline:
+    # P distinct non-depot locations per instance from a seeded permutation
+    torch.manual_seed(4321 + rank)
+    acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
+    fr = SLAPFusedEpisode(td, actions=acts, policy="teacher")
+    run = lambda: fr._launch(sh)  # noqa: E731
+    wall, ev = timed(run, 4 * k, 2, world, dev)
+    assert int(fr.status.item()) == 0
+    t = max_over_ranks(wall, world, dev)
+    out["slap_fused_random"] = {"value": world * b * 20 * 4 * k / t,
+                                "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
+                                "launch_us": ev / (4 * k) * 1e6, "bytes_per_episode": 2354,
+                                "achieved_GBps": b * 2354 / (ev / (4 * k)) / 1e9}
+    del fr, acts
     if not stepwise:
         return out
     ep = SLAPStepwiseEpisode(td, policy="closest").capture()

@@ -300,6 +300,58 @@ __device__ __forceinline__ void sort_keys(uint64_t (&k)[EPL]) {
 // (the int32 assignment keeps the raw value, slap/env.py:50-62).  The reward then runs
 // one lane per order over the LDS-staged assignment row and coordinates: K picks, the
 // closed pick tour in f32 in pick order, and the orders added in order by lane 0.
+// SLAP reward helpers: a pick's location (python wrap of the int32 assignment; -1 /
+// out of range -> flagged, location 0) and the closed tour of one order's KU picks in
+// pick order (f32, hardware sqrt: <= 1 ulp per edge, reward parity is 1e-5 relative).
+__device__ __forceinline__ float edge_len_hw(float x0, float y0, float x1, float y1) {
+  const float dx = x1 - x0, dy = y1 - y0;
+  return __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+}
+__device__ __forceinline__ int slap_pick_loc(int pp, const int32_t* asg, int L, bool& range) {
+  int64_t loc = 0;
+  if (pp < 0) {
+    range = true;
+  } else {
+    loc = asg[pp];
+    if (loc < 0) loc += L;
+    if (loc < 0 || loc >= L) {
+      range = true;
+      loc = 0;
+    }
+  }
+  return (int)loc;
+}
+template <int KU>
+__device__ __forceinline__ float slap_order_len(const int32_t* pk, const int32_t* asg,
+                                                const float2* xy, int L, bool& range,
+                                                int K = KU) {
+  int pp[KU], lc[KU];
+  float2 q[KU];
+#pragma unroll
+  for (int k = 0; k < KU; ++k) pp[k] = k < K ? pk[k] : 0;
+#pragma unroll
+  for (int k = 0; k < KU; ++k) lc[k] = k < K ? slap_pick_loc(pp[k], asg, L, range) : 0;
+#pragma unroll
+  for (int k = 0; k < KU; ++k) q[k] = xy[lc[k]];
+  float len = 0.f;
+#pragma unroll
+  for (int k = 1; k < KU; ++k)
+    if (k < K) len += edge_len_hw(q[k - 1].x, q[k - 1].y, q[k].x, q[k].y);
+  float2 ql = q[0];
+#pragma unroll
+  for (int k = 1; k < KU; ++k) ql = (k == K - 1) ? q[k] : ql;
+  return len + edge_len_hw(ql.x, ql.y, q[0].x, q[0].y);
+}
+
+__host__ __device__ inline size_t slap_asg_bytes(int ipb, int P) {
+  return ((size_t)ipb * P * 4 + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O, int K) {
+  const size_t keys = (size_t)epl * 64 * 8;
+  const size_t data = (size_t)gpw * (L * 8 + O * 4 + O * K * 4);
+  return ((keys > data ? keys : data) + 15) & ~(size_t)15;
+}
+
 template <int G, int EPL, bool CLOSEST>
 __global__ __launch_bounds__(256) void slap_group_kernel(
     int64_t B, int L, int P, int O, int K, const float2* __restrict__ locs,
@@ -309,20 +361,23 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
     int32_t* __restrict__ assign_out, int64_t* __restrict__ i_out, uint8_t* __restrict__ done_out,
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out,
     float* __restrict__ ratio_out, int32_t* status) {
-  constexpr int IPB = 256 / G;
+  constexpr int IPB = 256 / G, GPW = 64 / G;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float2* s_xy = reinterpret_cast<float2*>(smem);             // [IPB][L]
-  int32_t* s_asg = reinterpret_cast<int32_t*>(s_xy + IPB * L);  // [IPB][P]
-  float* s_len = reinterpret_cast<float*>(s_asg + IPB * P);     // [IPB][O]
-  int32_t* s_pk = reinterpret_cast<int32_t*>(s_len + IPB * O);  // [IPB][O*K] products
-  const int lane = lane_id(), sl = lane % G, g = threadIdx.x / G;
+  // [IPB][P] assignment rows, then one region per wave that holds the sorted candidate
+  // keys [EPL][64] during the step loop and, after it (same wave, program order), the
+  // coordinates [GPW][L], order lengths [GPW][O] and picklist products [GPW][O*K]
+  const int lane = lane_id(), sl = lane % G, g = threadIdx.x / G, gw = lane / G;
+  int32_t* s_asg = reinterpret_cast<int32_t*>(smem);
+  unsigned char* wreg = smem + slap_asg_bytes(IPB, P) +
+                        (size_t)(threadIdx.x >> 6) * slap_wave_bytes(GPW, EPL, L, O, K);
+  uint64_t* s_keys = reinterpret_cast<uint64_t*>(wreg);
   const int64_t b = (int64_t)blockIdx.x * IPB + g;
   const bool live = b < B;
   const int64_t bb = live ? b : 0;
-  float2* xy = s_xy + g * L;
+  float2* xy = reinterpret_cast<float2*>(wreg) + gw * L;
   int32_t* asg = s_asg + g * P;
-  float* olen = s_len + g * O;
-  int32_t* pks = s_pk + g * O * K;
+  float* olen = reinterpret_cast<float*>(wreg + (size_t)GPW * L * 8) + gw * O;
+  int32_t* pks = reinterpret_cast<int32_t*>(wreg + (size_t)GPW * (L * 8 + O * 4)) + gw * O * K;
 
   // Loads are issued in the order they are needed: the depot distances (the step loop),
   // then the coordinates and up to G*EPL picklist entries, which stay in registers during
@@ -337,6 +392,10 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
     if (ok) avail |= 1u << k;
     dd[k] = (CLOSEST && ok) ? depot_dist[bb * L + c] : __builtin_inff();
   }
+  // ratio (slap/env.py:114, zeros) depends on nothing: its stores go out first and
+  // drain while the loads are in flight
+  if (live && ratio_out)
+    for (int c = sl; c < L; c += G) ratio_out[bb * L + c] = 0.f;
   const float2* lrow = locs + bb * L;
   const int64_t* prow = picklist + bb * (int64_t)O * K;
   float2 xr[EPL];
@@ -352,6 +411,15 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
   // location); a step is then a group min over the lanes' heads and a pop by the owner,
   // instead of an EPL-wide scan + argmin and a slot clear.  A distance that is not below
   // +inf (taken, depot, pad, NaN) is never chosen; with no candidate left the action is 0.
+  // picklist entries as wrapped product indices (-1 = out of range), int32 before the
+  // step loop so the int64 loads do not stay live through it
+  auto wrap_product = [&](int64_t pp) -> int32_t {
+    if (pp < 0) pp += P;
+    return (pp < 0 || pp >= P) ? -1 : (int32_t)pp;
+  };
+  int32_t pw[EPL];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) pw[k] = wrap_product(pr[k]);
   uint64_t key[EPL];
   if (CLOSEST) {
 #pragma unroll
@@ -362,86 +430,146 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
     }
     sort_keys<EPL>(key);
   }
+#if defined(CO_SLAP_CUT) && CO_SLAP_CUT == 1
+  if (live && sl == 0 && (uint32_t)key[0] == 12345u + (uint32_t)pr[0] + (uint32_t)__float_as_uint(xr[0].x))
+    reward_out[bb] = 1.f;
+  return;
+#endif
   constexpr uint32_t kOrdInf = 0xff800000u;  // ordered key of +inf
   bool range = false;
-  for (int t = 0; t < P; ++t) {
-    int64_t a64;
-    if (CLOSEST) {
-      const uint32_t hh = (uint32_t)(key[0] >> 32);
+  if (CLOSEST) {
+    // The lane's head and next key stay in registers, the rest of its sorted list in
+    // LDS; a pop (owner lane only) is two moves and one LDS read that is waited for only
+    // at the lane's next pop.  The owner also clears its own free bit (the chosen
+    // location gi is slot gi / G of lane gi % G).
+    uint64_t hk = key[0], nk = EPL > 1 ? key[1] : ~0ull;
+#pragma unroll
+    for (int k = 2; k < EPL; ++k) s_keys[k * 64 + lane] = key[k];
+    int h = 2;
+    for (int t = 0; t < P; ++t) {
+      const uint32_t hh = (uint32_t)(hk >> 32);
       const uint32_t gm = grp_reduce<G>(hh, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
-      const uint32_t cand = hh == gm ? (uint32_t)key[0] : 0xffffffffu;
+      const uint32_t cand = hh == gm ? (uint32_t)hk : 0xffffffffu;
       const uint32_t gi =
           grp_reduce<G>(cand, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
       const bool any = gm < kOrdInf;
-      a64 = any ? (int64_t)gi : 0;
-      if (any && sl == (int)(gi % G)) {  // the owner's head is the chosen location
-#pragma unroll
-        for (int k = 0; k < EPL - 1; ++k) key[k] = key[k + 1];
-        key[EPL - 1] = ~0ull;
+      if (any && (uint32_t)hk == gi) {  // the owner's head is the chosen location
+        avail &= ~(1u << (gi / G));
+        hk = nk;
+        nk = h < EPL ? s_keys[h * 64 + lane] : ~0ull;
+        ++h;
       }
-      if (live && sl == 0) acts_out[(int64_t)t * B + bb] = a64;
-    } else {
-      a64 = acts_in[(int64_t)t * B + bb];
+      if (sl == 0) asg[t] = any ? (int32_t)gi : 0;  // product t
     }
-    if (sl == 0) asg[t] = (int32_t)a64;  // product t
-    const int64_t a = a64 < 0 ? a64 + L : a64;
-    if (a < 0 || a >= L) {
-      range = true;
-    } else if (sl == (int)(a % G)) {
-      avail &= ~(1u << (int)(a / G));
+  } else {
+    // teacher actions: lane sl loads steps t = sl, sl + G, ... (all loads in flight at
+    // once, a few VGPRs), writes the int32 assignment entry and the wrapped location (-1
+    // when out of range) to LDS; after a wave fence every lane scans the P locations for
+    // the free bits it owns.  The wrapped locations use the wave's key region (unused by
+    // the teacher path); P*GPW ints always fit it for P <= 256.
+    int32_t* s_w = reinterpret_cast<int32_t*>(wreg) + gw * P;
+    if (P * GPW <= EPL * 128) {
+#pragma unroll 4
+      for (int t = sl; t < P; t += G) {
+        const int64_t a64 = acts_in[(int64_t)t * B + bb];
+        asg[t] = (int32_t)a64;  // product t
+        const int64_t a = a64 < 0 ? a64 + L : a64;
+        const bool bad = a < 0 || a >= L;
+        range |= bad;
+        s_w[t] = bad ? -1 : (int)a;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int t = 0; t < P; ++t) {
+        const int a = s_w[t];
+        if (a >= 0 && sl == a % G) avail &= ~(1u << (a / G));
+      }
+    } else {
+      for (int t = 0; t < P; ++t) {
+        const int64_t a64 = acts_in[(int64_t)t * B + bb];
+        if (sl == 0) asg[t] = (int32_t)a64;  // product t
+        const int64_t a = a64 < 0 ? a64 + L : a64;
+        if (a < 0 || a >= L) {
+          range = true;
+        } else if (sl == (int)(a % G)) {
+          avail &= ~(1u << (int)(a / G));
+        }
+      }
     }
   }
+#if defined(CO_SLAP_CUT) && CO_SLAP_CUT == 2
+  {
+    uint32_t sink = avail;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k)
+      sink += (uint32_t)pw[k] + __float_as_uint(xr[k].x) + __float_as_uint(xr[k].y);
+    if (live && sink == 12345u) reward_out[bb] = 1.f;
+    return;
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
     const int c = sl + G * k;
     if (c < L) xy[c] = xr[k];
   }
   // picklist entries as wrapped product indices (-1 = out of range)
-  for (int c = sl; c < O * K; c += G) {
-    int64_t pp = c < G * EPL ? pr[0] : prow[c];
 #pragma unroll
-    for (int k = 1; k < EPL; ++k) pp = (c == sl + G * k) ? pr[k] : pp;
-    if (pp < 0) pp += P;
-    pks[c] = (pp < 0 || pp >= P) ? -1 : (int32_t)pp;
+  for (int k = 0; k < EPL; ++k) {  // entry sl + G*k is register pw[k]
+    const int c = sl + G * k;
+    if (c < O * K) pks[c] = pw[k];
   }
+  for (int c = sl + G * EPL; c < O * K; c += G) pks[c] = wrap_product(prow[c]);
   // the group's LDS rows are written and read by lanes of the same wave: a wave-level
   // fence orders them, no workgroup barrier (groups do not wait for other waves)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+  // closest policy: the step-major action rows of the wave's 64/G instances, written
+  // once from the LDS assignment rows (P x 64/G int64 values, 2 store instructions
+  // instead of one per step)
+  if (CLOSEST) {
+    constexpr int IPW = 64 / G;
+    const int w0 = (threadIdx.x >> 6) * IPW;  // first group of this wave
+    for (int idx = lane; idx < IPW * P; idx += 64) {
+      const int t = idx / IPW, gi = idx - t * IPW;
+      const int64_t be = (int64_t)blockIdx.x * IPB + w0 + gi;
+      if (be < B) acts_out[(int64_t)t * B + be] = s_asg[(w0 + gi) * P + t];
+    }
+  }
+  // one lane per order; for K <= 8 the K picks' LDS lookups (product -> location ->
+  // coordinates) are three independent batches, not a K-long dependent chain
   for (int o = sl; o < O; o += G) {
     const int32_t* pk = pks + o * K;
-    float2 p0 = make_float2(0.f, 0.f), prev = p0;
     float len = 0.f;
-    for (int k = 0; k < K; ++k) {
-      const int pp = pk[k];
-      int64_t loc = 0;
-      if (pp < 0) {
-        range = true;
-      } else {
-        loc = asg[pp];
-        if (loc < 0) loc += L;
-        if (loc < 0 || loc >= L) {
-          range = true;
-          loc = 0;
+    if (K == 5) {  // examples/slap.py: max_products_in_order = 5
+      len = slap_order_len<5>(pk, asg, xy, L, range);
+    } else if (K <= 8) {
+      len = slap_order_len<8>(pk, asg, xy, L, range, K);
+    } else {
+      float2 p0 = make_float2(0.f, 0.f), prev = p0;
+      for (int k = 0; k < K; ++k) {
+        const float2 q = xy[slap_pick_loc(pk[k], asg, L, range)];
+        if (k == 0) {
+          p0 = q;
+        } else {
+          len += edge_len_hw(prev.x, prev.y, q.x, q.y);
         }
+        prev = q;
       }
-      const float2 q = xy[loc];
-      if (k == 0) {
-        p0 = q;
-      } else {
-        len += edge_len(prev.x, prev.y, q.x, q.y);
-      }
-      prev = q;
+      len += edge_len_hw(prev.x, prev.y, p0.x, p0.y);
     }
-    len += edge_len(prev.x, prev.y, p0.x, p0.y);
     olen[o] = len;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+#if defined(CO_SLAP_CUT) && CO_SLAP_CUT == 3
+  if (live && sl == 0) reward_out[bb] = olen[0] + (float)avail;
+  return;
+#endif
   if (live) {
     uint8_t* mrow = mask_out + bb * L;
 #pragma unroll
@@ -450,8 +578,6 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
       if (c < L) mrow[c] = (avail >> k) & 1u;
     }
     for (int c = sl; c < P; c += G) assign_out[bb * P + c] = asg[c];
-    if (ratio_out)
-      for (int c = sl; c < L; c += G) ratio_out[bb * L + c] = 0.f;
     if (sl == 0) {
       // f32 order-by-order accumulation of slap/env.py:135-142
       float total = 0.f;
@@ -547,7 +673,8 @@ extern "C" int co_slap_rollout(int64_t B, int64_t L, int64_t P, int64_t O, int64
   // 8 lanes 33 us, 32 lanes 38 us, at B = 16,384)
   const int G = L <= 64 ? 8 : (L <= 128 ? 16 : 32);
   const int ipb = 256 / G;
-  const size_t shmem = (size_t)ipb * (L * 8 + P * 4 + O * 4 + O * K * 4);
+  const size_t shmem =
+      slap_asg_bytes(ipb, (int)P) + 4 * slap_wave_bytes(64 / G, 8, (int)L, (int)O, (int)K);
   if (shmem > 160 * 1024) return CO_E_INVAL;
   const dim3 grid((unsigned)((B + ipb - 1) / ipb)), block(256);
   hipStream_t s = (hipStream_t)stream;

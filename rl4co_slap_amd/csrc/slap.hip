@@ -146,7 +146,8 @@ __global__ __launch_bounds__(256) void slap_closest_kernel(int64_t B, int L, con
     float best = __builtin_inff();
     int bi = 0x7fffffff;
     for (int c = lane; c < L; c += 64) {
-      const float d = mrow[c] ? drow[c] : __builtin_inff();
+      const float dv = drow[c];  // unconditional: a load behind the mask test is serialised
+      const float d = mrow[c] ? dv : __builtin_inff();
       if (d < best || (d == best && c < bi)) { best = d; bi = c; }
     }
     wave_argmin(best, bi);

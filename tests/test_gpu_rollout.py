@@ -132,6 +132,43 @@ def test_slap_rollout_matches_oracle(dev, cls_name, b, policy):
     assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
 
 
+@pytest.mark.parametrize("aisles,locs,prods,orders", [(6, 8, 12, 9), (12, 15, 40, 25),
+                                                      (10, 10, 20, 20), (4, 5, 19, 7)])
+@pytest.mark.parametrize("dist", ["grid", "random_ties"])
+def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist):
+    """Fused closest-free episode for every lane-group width (L = 48 -> 8 lanes, 100 -> 16,
+    180 -> 32), P close to L - 1 (a lane's sorted list runs dry), and depot distances
+    with many exact ties at random positions."""
+    import numpy as np
+
+    from oracle.envs import SLAPOracle, slap_closest_free_action
+    from oracle.td import TD
+    from rl4co_slap_amd.rollout.engine import SLAPFusedEpisode
+    from rl4co_slap_amd.td import TensorDict
+
+    b = 77
+    env = SLAPOracle(n_products=prods, n_aisles=aisles, n_locs=locs, max_orders=orders, seed=3)
+    np.random.seed(3)
+    gen = env.generate([b])
+    if dist == "random_ties":
+        g = torch.Generator().manual_seed(9)
+        gen["depot_loc_dist"] = torch.randint(0, 6, gen["depot_loc_dist"].shape,
+                                              generator=g).float() * 0.5
+    td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    r, tdf, a = ref_rollout(env, td, slap_closest_free_action)
+    ep = SLAPFusedEpisode(TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev),
+                          None, policy="closest")
+    ep.run_eager()
+    torch.cuda.synchronize()
+    assert int(ep.status.item()) == 0
+    st = ep.final_state()
+    assert torch.equal(st["actions"].cpu(), a)
+    for k in ("action_mask", "i", "assignment", "done"):
+        assert torch.equal(st[k].cpu(), tdf[k]), k
+    got = st["reward"].cpu()
+    assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
+
+
 # --------------------------------------------------------------------------- CVRP
 def _cvrp_ref(b, n, seed):
     from oracle.envs import CVRPOracle, cvrp_nearest_action

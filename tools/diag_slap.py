@@ -21,7 +21,12 @@ for b in (16384, 65536):
     torch.manual_seed(1234)
     np.random.seed(1234)
     td = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
-    fu = SLAPFusedEpisode(td, policy="closest")
+    pol = os.environ.get("DIAG_POLICY", "closest")
+    acts = None
+    if pol == "teacher":
+        torch.manual_seed(4321)
+        acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
+    fu = SLAPFusedEpisode(td, actions=acts, policy=pol)
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -41,5 +46,5 @@ for b in (16384, 65536):
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / 20
-    print(f"SLAP fused closest B={b}: {us:.1f} us  {b * 2754 / us / 1e3:.0f} GB/s "
+    print(f"SLAP fused {pol} B={b}: {us:.1f} us  {b * 2754 / us / 1e3:.0f} GB/s "
           f"status={int(fu.status.item())} reward_sum={float(fu.reward.sum()):.3f}")
