@@ -77,18 +77,38 @@ def test_tsp_fused_full_size_properties(dev):
     assert (st["i"] == n).all()
     assert torch.equal(st["first_node"].cpu(), acts[:, 0])
     assert torch.equal(st["current_node"].cpu(), acts[:, -1])
-    # spot-check 512 random instances against the oracle reward
-    idx = torch.randperm(b, generator=g)[:512]
+    # every instance's reward against the oracle's tour length
     from oracle.ops import gather_by_index, get_tour_length
 
-    ref = -get_tour_length(gather_by_index(locs[idx], acts[idx]))
-    got = st["reward"].cpu()[idx]
+    ref = -get_tour_length(gather_by_index(locs, acts))
+    got = st["reward"].cpu()
     assert ((got - ref).abs() <= 1e-5 * ref.abs().clamp(min=1)).all()
     # rotation invariance of the closed tour length
     ep2 = TSPFusedEpisode(locs.to(dev), acts.roll(37, dims=1).to(dev))
     ep2.run_eager()
     torch.cuda.synchronize()
     assert ((ep2.reward - ep.reward).abs() <= 1e-5 * ep.reward.abs()).all()
+
+
+@pytest.mark.parametrize("bad", [5, 64 * 700 + 47, 64 * 700 + 48, 64 * 1000 + 63])
+def test_tsp_fused_large_batch_invalid_tour_flag(dev, bad):
+    """Revisit detection at the full batch (1.33 rounds of resident tiles: first-round and
+    tail tiles, low and high lanes), other instances' rewards unaffected."""
+    b, n = 64 * 1024, 100
+    locs = torch.rand(b, n, 2, generator=torch.Generator().manual_seed(7))
+    acts = torch.arange(n).repeat(b, 1)
+    acts[bad, 60] = 3  # node 3 twice, node 60 never
+    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep.run_eager()
+    torch.cuda.synchronize()
+    assert int(ep.status.item()) & 1
+    from oracle.ops import gather_by_index, get_tour_length
+
+    ok = torch.ones(b, dtype=torch.bool)
+    ok[bad] = False
+    ref = -get_tour_length(gather_by_index(locs[ok], acts[ok]))
+    got = ep.reward.cpu()[ok]
+    assert ((got - ref).abs() <= 1e-5 * ref.abs().clamp(min=1)).all()
 
 
 def _slap_ref(b, seed, policy):

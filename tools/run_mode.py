@@ -24,6 +24,8 @@ def main():
     torch.cuda.set_device(dev)
     from rl4co_slap_amd import _native
 
+    if os.environ.get("CO_LIB"):  # a variant library (tools/build_variants.sh)
+        _native.LIB_PATH = os.environ["CO_LIB"]
     _native.load()
     if a.mode == "cvrp":
         out = bench.bench_cvrp(32768, 100, a.k, 1, 0, dev)
