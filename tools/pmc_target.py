@@ -28,13 +28,17 @@ if args.kernel.startswith("tsp"):
         ep = engine.TSPFusedEpisode(locs.to(dev), None, policy="nearest")
     else:
         ep = engine.TSPStepwiseEpisode(locs.to(dev), acts.to(dev))
-elif args.kernel == "cvrp_fused_nearest":
+elif args.kernel.startswith("cvrp"):
     torch.manual_seed(1234)
     locs_all = torch.rand(32768, 101, 2)
     demand = ((torch.rand(32768, 100) * 9).int() + 1).float() / 50.0
-    ep = engine.CVRPFusedEpisode({"depot": locs_all[:, 0].contiguous().to(dev),
-                                  "locs": locs_all[:, 1:].contiguous().to(dev),
-                                  "demand": demand.to(dev)})
+    td = {"depot": locs_all[:, 0].contiguous().to(dev),
+          "locs": locs_all[:, 1:].contiguous().to(dev), "demand": demand.to(dev)}
+    if args.kernel == "cvrp_fused_nearest":
+        ep = engine.CVRPFusedEpisode(td)
+    else:  # cvrp_stepwise: the graph-chunked reference loop (replay = one episode)
+        ep = engine.CVRPStepwiseEpisode(td).capture()
+        ep.run_eager = ep.replay
 elif args.kernel == "pomo_tsp100":
     from rl4co_slap_amd.rollout.pomo import POMOEpisode
 
@@ -50,8 +54,14 @@ else:
 
     torch.manual_seed(1234)
     np.random.seed(1234)
-    td = SLAPGenerator(materialize_dist_mat=False)(16384).to(dev)
-    ep = engine.SLAPFusedEpisode(td, None, policy="closest")
+    b = 65536 if args.kernel.endswith("b65536") else 16384
+    td = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
+    if args.kernel.startswith("slap_fused_random"):
+        torch.manual_seed(4321)
+        acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
+        ep = engine.SLAPFusedEpisode(td, acts, policy="teacher")
+    else:
+        ep = engine.SLAPFusedEpisode(td, None, policy="closest")
 for _ in range(args.k):
     ep.run_eager()
 torch.cuda.synchronize()
