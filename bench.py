@@ -20,6 +20,7 @@ CPU oracle (plain-PyTorch restatement of the reference op sequence) on this host
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -99,12 +100,53 @@ def timed(run, steps, warmup, world, dev):
     return time.perf_counter() - t0, ev0.elapsed_time(ev1) / 1e3
 
 
-def tsp_inputs(b, n, rank):
-    torch.manual_seed(1234 + rank)
+def tsp_inputs(b, n, rank, salt=0):
+    torch.manual_seed(1234 + rank + 104729 * salt)
     locs = torch.rand(b, n, 2)
-    torch.manual_seed(4321 + rank)
+    torch.manual_seed(4321 + rank + 104729 * salt)
     acts = torch.rand(b, n).argsort(1)
     return locs, acts
+
+
+MALL_BYTES = 256 << 20  # Infinity Cache (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def rotation(input_bytes):
+    """Distinct input batches a timed loop cycles through so that no launch finds its
+    inputs Infinity-Cache resident from their previous use: together they exceed the
+    256 MiB cache by 25 % (a cyclic sweep larger than an LRU cache misses every line), so
+    the rates below are HBM rates.  (One batch repeated would stay resident: 105 MB of
+    TSP-100 inputs at B = 65,536.)"""
+    return max(2, min(16, -(-int(1.25 * MALL_BYTES) // max(1, int(input_bytes)))))
+
+
+def copy_probe(traffic_bytes, dev, k):
+    """The streaming ceiling beside the roofline: co_probe_copy (16-B loads and stores)
+    moving the same HBM bytes as one headline launch (source buffers cycled past the
+    Infinity Cache), and 2 GiB (asymptotic)."""
+    from rl4co_slap_amd import _native as nat
+
+    res = {}
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for label, traffic in (("same_bytes", traffic_bytes), ("2GiB", 2 << 30)):
+        n = (traffic // 2) // 16 * 16
+        r = rotation(n) if n < MALL_BYTES else 1
+        bufs = [(torch.ones(n, dtype=torch.uint8, device=dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(r)]
+        fs = [nat.bind("co_probe_copy", nat.ptr(a), nat.ptr(c), n) for a, c in bufs]
+        for f in fs:
+            f(s)
+        reps = max(k, 10, r)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            fs[i % r](s)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        t = e0.elapsed_time(e1) / 1e3 / reps
+        res[label] = {"bytes": 2 * n, "us": t * 1e6, "GBps": 2 * n / t / 1e9, "buffers_cycled": r}
+        del bufs, fs
+    return res
 
 
 def cpu_threads():
@@ -219,11 +261,19 @@ def main():
     locs, acts = locs_cpu.to(dev), acts_cpu.to(dev)
 
     # ---- headline: fused one-launch episode, eager back-to-back launches ---------------
-    ep = TSPFusedEpisode(locs, acts, policy="teacher", check=True)
+    # distinct batches cycled (16 B of inputs per node and instance): every launch reads
+    # its inputs from HBM, not from the Infinity Cache after the previous launch
+    n_rot = rotation(b * n * 16)
+    eps = [TSPFusedEpisode(locs, acts, policy="teacher", check=True)]
+    for r in range(1, n_rot):
+        lr, ar = tsp_inputs(b, n, rank, salt=r)
+        eps.append(TSPFusedEpisode(lr.to(dev), ar.to(dev), policy="teacher", check=True))
     sh = torch.cuda.current_stream(dev).cuda_stream  # launch stream, looked up once
-    s = lambda: ep._launch(sh)  # noqa: E731
+    cyc = itertools.cycle([e._bound for e in eps])
+    s = lambda: next(cyc)(sh)  # noqa: E731
     wall, ev = timed(s, args.steps, args.warmup, world, dev)
-    assert int(ep.status.item()) == 0, "invalid tour in the benchmark episode"
+    assert all(int(e.status.item()) == 0 for e in eps), "invalid tour in the benchmark episode"
+    del eps
     t = max_over_ranks(wall, world, dev)
     value = world * b * n * args.steps / t
     per_launch = ev / args.steps
@@ -247,8 +297,10 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "bytes_per_launch": bytes_per_launch, "launch_us": per_launch * 1e6},
+                     "bytes_per_launch": bytes_per_launch, "launch_us": per_launch * 1e6,
+                     "copy_probe": copy_probe(bytes_per_launch, dev, args.steps)},
     }
+    out["config"]["input_batches_cycled"] = n_rot
 
     if not args.no_modes:
         modes = {}
@@ -334,34 +386,40 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
     np.random.seed(1234 + rank)
     from rl4co_slap_amd.rollout.engine import SLAPFusedEpisode
 
-    td = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
+    gen = SLAPGenerator(materialize_dist_mat=False)
+    n_rot = rotation(b * 2000)  # locs 8L + picklist 8OK + depot distances 4L per instance
+    tds = [gen(b).to(dev) for _ in range(n_rot)]
+    td = tds[0]
     out = {}
-    fu = SLAPFusedEpisode(td, policy="closest")
+    fus = [SLAPFusedEpisode(t, policy="closest") for t in tds]
     sh = torch.cuda.current_stream(dev).cuda_stream
-    run = lambda: fu._launch(sh)  # noqa: E731
+    cyc = itertools.cycle([f._bound for f in fus])
+    run = lambda: next(cyc)(sh)  # noqa: E731
     wall, ev = timed(run, 4 * k, 2, world, dev)
-    assert int(fu.status.item()) == 0
+    assert all(int(f.status.item()) == 0 for f in fus)
     t = max_over_ranks(wall, world, dev)
     out["slap_fused_closest"] = {"value": world * b * 20 * 4 * k / t,
                                  "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
                                  "launch_us": ev / (4 * k) * 1e6,
-                                 "bytes_per_episode": 2754,
+                                 "bytes_per_episode": 2754, "input_batches_cycled": n_rot,
                                  "achieved_GBps": b * 2754 / (ev / (4 * k)) / 1e9}
-    del fu
+    del fus
     # random-feasible policy, teacher-forced like the TSP headline:
     # P distinct non-depot locations per instance from a seeded permutation
     torch.manual_seed(4321 + rank)
-    acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
-    fr = SLAPFusedEpisode(td, actions=acts, policy="teacher")
-    run = lambda: fr._launch(sh)  # noqa: E731
+    frs = [SLAPFusedEpisode(t, actions=(torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev),
+                            policy="teacher") for t in tds]
+    cyc = itertools.cycle([f._bound for f in frs])
+    run = lambda: next(cyc)(sh)  # noqa: E731
     wall, ev = timed(run, 4 * k, 2, world, dev)
-    assert int(fr.status.item()) == 0
+    assert all(int(f.status.item()) == 0 for f in frs)
     t = max_over_ranks(wall, world, dev)
     out["slap_fused_random"] = {"value": world * b * 20 * 4 * k / t,
                                 "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
                                 "launch_us": ev / (4 * k) * 1e6, "bytes_per_episode": 2354,
+                                "input_batches_cycled": n_rot,
                                 "achieved_GBps": b * 2354 / (ev / (4 * k)) / 1e9}
-    del fr, acts
+    del frs
     if not stepwise:
         return out
     ep = SLAPStepwiseEpisode(td, policy="closest").capture()
@@ -384,23 +442,38 @@ def bench_cvrp(b, n, k, world, rank, dev):
     td = {"depot": locs_all[:, 0].contiguous().to(dev), "locs": locs_all[:, 1:].contiguous().to(dev),
           "demand": demand.to(dev)}
     out = {}
-    fu = CVRPFusedEpisode(td)
+    # batches cycled past the Infinity Cache, each launched equally often (T differs per batch)
+    n_rot = rotation(b * (12 * n + 8))
+    tds = [td]
+    for _ in range(1, n_rot):
+        la = torch.rand(b, n + 1, 2)
+        dm = ((torch.rand(b, n) * 9).int() + 1).float() / 50.0
+        tds.append({"depot": la[:, 0].contiguous().to(dev), "locs": la[:, 1:].contiguous().to(dev),
+                    "demand": dm.to(dev)})
+    fus = [CVRPFusedEpisode(x) for x in tds]
     sh = torch.cuda.current_stream(dev).cuda_stream
-    run = lambda: fu._launch(sh)  # noqa: E731
-    wall, ev = timed(run, 4 * k, 2, world, dev)
-    st = fu.final_state()
-    T = st["steps"]
+    cyc = itertools.cycle([f._bound for f in fus])
+    run = lambda: next(cyc)(sh)  # noqa: E731
+    kk = n_rot * max(1, (4 * k) // n_rot)
+    wall, ev = timed(run, kk, n_rot, world, dev)
+    Ts = [f.final_state()["steps"] for f in fus]
+    T = Ts[0]
     t = max_over_ranks(wall, world, dev)
-    steps_all = sum_over_ranks(b * T, world, dev)  # T differs per rank (own instances)
-    out["cvrp_fused_nearest"] = {"value": steps_all * 4 * k / t,
-                                 "ms_per_episode": t / (4 * k) * 1e3, "batch_per_gpu": b,
+    # env-steps = B x T per launch, T the batch-wide length of that batch's episode
+    steps_all = sum_over_ranks(b * sum(Ts) * (kk // n_rot), world, dev)
+    out["cvrp_fused_nearest"] = {"value": steps_all / t,
+                                 "ms_per_episode": t / kk * 1e3, "batch_per_gpu": b,
                                  "num_loc": n, "episode_steps": T,
-                                 "launch_us": ev / (4 * k) * 1e6}
+                                 "episode_steps_mean": sum(Ts) / n_rot,
+                                 "input_batches_cycled": n_rot,
+                                 "launch_us": ev / kk * 1e6}
+    del fus
     sw = CVRPStepwiseEpisode(td).capture()
     wall, ev = timed(sw.replay, k, 1, world, dev)
     t = max_over_ranks(wall, world, dev)
     assert sw.T == T
-    out["cvrp_stepwise_graph"] = {"value": steps_all * k / t, "ms_per_episode": t / k * 1e3,
+    steps_one = sum_over_ranks(b * T, world, dev)
+    out["cvrp_stepwise_graph"] = {"value": steps_one * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "episode_steps": T,
                                   "bytes_per_env_step": 7 * n + 33}
     return out

@@ -324,6 +324,12 @@ int co_distance_matrix(int64_t batch, int64_t num_loc, const float* locs, float*
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 
+/* ------------------------------------------------ measurement utility (no reference
+ * counterpart): dst[0:nbytes) = src[0:nbytes), one 16-byte load/store per thread over a
+ * full grid -- the streaming ceiling the bench quotes beside each kernel's roofline.
+ * src/dst 16-byte aligned, nbytes a multiple of 16. */
+int co_probe_copy(const void* src, void* dst, int64_t nbytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -498,13 +498,26 @@ extern "C" int co_cvrp_reward(int64_t B, int64_t N, int64_t T, const float* locs
   if (check && (!demand || !vcap || !status)) return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
   const size_t per_wave = check ? (size_t)((N + 32) / 32 + T) * 4 : 0;
-  int waves = 4;
+  // step-major actions ([T, B] rows): 16 consecutive instances per workgroup, so each
+  // 128-B line of an action row is consumed on one CU (4 per workgroup spread a line over
+  // 4 XCDs' L2s: 160 MB read per launch at B = 32,768, T = 112, vs ~70 MB algorithmic)
+  int waves = (sb == 1 && st == B) ? 16 : 4;
   while (waves > 1 && per_wave * waves > 64 * 1024) waves >>= 1;
   if (per_wave > 64 * 1024) return CO_E_INVAL;
   const size_t shmem = per_wave * waves;
   const dim3 grid(grid_for(B, waves, 256 * 32));
   const float2* l2 = reinterpret_cast<const float2*>(locs);
   switch (waves) {
+    case 16:
+      hipLaunchKernelGGL(cvrp_reward_kernel<16>, grid, dim3(1024), shmem, (hipStream_t)stream,
+                         B, (int)N, (int)T, l2, actions, sb, st, demand, vcap, check, reward,
+                         status);
+      break;
+    case 8:
+      hipLaunchKernelGGL(cvrp_reward_kernel<8>, grid, dim3(512), shmem, (hipStream_t)stream, B,
+                         (int)N, (int)T, l2, actions, sb, st, demand, vcap, check, reward,
+                         status);
+      break;
     case 4:
       hipLaunchKernelGGL(cvrp_reward_kernel<4>, grid, dim3(256), shmem, (hipStream_t)stream, B,
                          (int)N, (int)T, l2, actions, sb, st, demand, vcap, check, reward,

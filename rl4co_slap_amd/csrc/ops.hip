@@ -177,6 +177,30 @@ extern "C" int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count,
   return launch_status();
 }
 
+// ------------------------------------------------------------------ measurement probe
+namespace {
+// one 16-B unit per thread over a full grid (the float4-copy shape of the guide's 6.29 TB/s
+// measurement; grid-stride variants with 1 or 4 units in flight measured 5.07 / 4.25 TB/s)
+__global__ __launch_bounds__(256) void probe_copy_kernel(const uint4* __restrict__ src,
+                                                         uint4* __restrict__ dst, int64_t n16) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+}
+}  // namespace
+
+extern "C" int co_probe_copy(const void* src, void* dst, int64_t nbytes, void* stream) {
+  if (nbytes < 0 || (nbytes & 15) || (nbytes > 0 && (!src || !dst))) return CO_E_INVAL;
+  if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) != 0)
+    return CO_E_ALIGN;
+  if (nbytes == 0) return CO_OK;
+  const int64_t blocks = (nbytes / 16 + 255) / 256;
+  if (blocks > 0x7fffffff) return CO_E_INVAL;
+  hipLaunchKernelGGL(probe_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst),
+                     nbytes / 16);
+  return launch_status();
+}
+
 // ------------------------------------------------------------------ augmentation
 // data/transforms.py:15-37 dihedral_8_augmentation: out[r*B*N + i] = transform r of
 // in[i] (i = b*N + c), r = 0..7 in the reference's order z0..z7; the [8B, N, 2] output is
