@@ -18,14 +18,6 @@ namespace {
 
 constexpr int kNoNode = 0x7fffffff;
 
-template <int EPL>
-__device__ __forceinline__ float pick(const float (&v)[EPL], int slot) {
-  float r = 0.f;
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) r = (k == slot) ? v[k] : r;
-  return r;
-}
-
 // Lane-local nearest candidate: argmin over the candidates (bit k of `cand`) of the f32
 // distance sqrt(dx*dx + dy*dy), ties -> lowest node index, exactly as torch.argmin over
 // the oracle's distances.  The scan compares squared distances (the same IEEE products
@@ -38,24 +30,22 @@ __device__ __forceinline__ void lane_nearest(float cx, float cy, const float (&p
                                              const float (&py)[EPL], uint32_t cand, int sl,
                                              float& best, int& bi) {
   float sq[EPL];
-  float smin = __builtin_inff();
+  float smin = __builtin_inff(), sbef = __builtin_inff();
   int kmin = -1;
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
     const float dx = px[k] - cx, dy = py[k] - cy;
     sq[k] = dx * dx + dy * dy;
-    if (((cand >> k) & 1u) && sq[k] < smin) {
-      smin = sq[k];
-      kmin = k;
-    }
+    const bool take = ((cand >> k) & 1u) && sq[k] < smin;
+    sbef = take ? smin : sbef;  // running min of the candidates before the new best
+    smin = take ? sq[k] : smin;
+    kmin = take ? k : kmin;
   }
   best = kmin >= 0 ? sqrtf(smin) : __builtin_inff();
   bi = kmin >= 0 ? sl + G * kmin : kNoNode;
   const float win = smin * (1.0f + 0x1p-20f);
-  bool need = false;
-#pragma unroll
-  for (int k = 0; k < EPL; ++k) need |= ((cand >> k) & 1u) && k < kmin && sq[k] <= win;
-  if (need) {  // rare: an earlier node whose distance rounds to the same sqrt
+  // sbef = min over the candidates with k < kmin: one compare instead of an EPL-wide test
+  if (kmin >= 0 && sbef <= win) {  // rare: an earlier node whose distance rounds to the same sqrt
     int kk = kmin;
 #pragma unroll
     for (int k = EPL - 1; k >= 0; --k)
@@ -72,7 +62,11 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
     int64_t* __restrict__ cur_out, int64_t* __restrict__ i_out, uint8_t* __restrict__ done_out,
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out) {
   constexpr int IPW = 64 / G;
-  const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
+  // the group's coordinate row in LDS: the chosen node's coordinates are one broadcast
+  // ds_read per step instead of an EPL-wide register select and two lane shuffles
+  __shared__ float2 s_xy[256 * EPL];
+  const int lane = lane_id(), sl = lane % G;
+  float2* xyg = s_xy + (threadIdx.x / G) * (G * EPL);
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   for (int64_t base = wid * IPW; base < B; base += nwaves * IPW) {
@@ -88,10 +82,16 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
       const float2 q = c < N ? lrow[c] : make_float2(0.f, 0.f);
       px[k] = q.x;
       py[k] = q.y;
+      xyg[c] = q;
       if (c >= N) vis |= 1u << k;
     }
+    // the row is written and read by lanes of this wave only: a wave-level fence
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (sl == 0) vis |= 1u;  // step 0: node 0
-    const float x0 = __shfl(px[0], gbase, 64), y0 = __shfl(py[0], gbase, 64);
+    const float2 p0 = xyg[0];
+    const float x0 = p0.x, y0 = p0.y;
     float cx = x0, cy = y0;
     if (valid && sl == 0) acts_out[bb] = 0;
     double len = 0.0;
@@ -103,13 +103,18 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
       grp_argmin_split<G>(best, bi);  // t < N: an unvisited node remains
       const int owner = bi % G, slot = bi / G;
       if (sl == owner) vis |= 1u << slot;
-      cx = __shfl(pick(px, slot), gbase + owner, 64);
-      cy = __shfl(pick(py, slot), gbase + owner, 64);
+      const float2 q = xyg[bi];
+      cx = q.x;
+      cy = q.y;
       len += (double)best;
       cur = bi;
       if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = bi;
     }
     len += (double)edge_len(cx, cy, x0, y0);
+    // the next instance's row overwrites this one: order the reads above before it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (!valid) continue;
     uint8_t* mrow = mask_out + bb * N;
     for (int c = sl; c < N; c += G) mrow[c] = 0;  // every node visited
@@ -140,7 +145,10 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out,
     int32_t* __restrict__ len_out, int32_t* __restrict__ tmax, int32_t* status) {
   constexpr int IPW = 64 / G;
+  // the group's nodes (x, y, demand) in LDS: the chosen node is one broadcast ds_read
+  __shared__ float4 s_node[256 * EPL];
   const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
+  float4* ndg = s_node + (threadIdx.x / G) * (G * EPL);
   const int M = N + 1;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -167,9 +175,13 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
       px[k] = q.x;
       py[k] = q.y;
       dm[k] = d;
+      ndg[c] = make_float4(q.x, q.y, d, 0.f);
       if (c > N) vis |= 1u << k;
       if (valid && locs_out && c <= N) locs_out[bb * M + c] = q;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float cx = dep.x, cy = dep.y, used = 0.f;
     int cur = 0, ncust = 0, len = 0;
     bool depot_seen = false, done = false;
@@ -190,9 +202,8 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
       if (done) continue;
       const int a = bi == kNoNode ? 0 : bi;
       const int owner = a % G, slot = a / G;
-      const float ax = __shfl(pick(px, slot), gbase + owner, 64);
-      const float ay = __shfl(pick(py, slot), gbase + owner, 64);
-      const float ad = __shfl(pick(dm, slot), gbase + owner, 64);
+      const float4 nd = ndg[a];
+      const float ax = nd.x, ay = nd.y, ad = nd.z;
       if (sl == owner) vis |= 1u << slot;
       dist += (double)(a == 0 ? edge_len(cx, cy, ax, ay) : best);
       used = a != 0 ? (used + ad) * 1.0f : 0.0f;  // cvrp/env.py:83-85
@@ -206,6 +217,9 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
       done = ncust == N && depot_seen;
     }
     dist += (double)edge_len(cx, cy, dep.x, dep.y);  // closing edge to the depot
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // next row overwrites this one
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // final state rows: visited and get_action_mask (cvrp/env.py:137-149)
     bool any_feas = false;
     uint8_t* vrow = visited_out + bb * M;
