@@ -116,8 +116,14 @@ __global__ __launch_bounds__(256) void cvrp_step_kernel(
 // depot byte of each row is patched into its chunk after the barrier, so every byte of
 // the mask tile is written once by a 16-B store.  `not_done` (optional) receives one
 // atomicAdd per workgroup: the number of its rows that are not done.
-constexpr int kCvrpCpt = 2;
-constexpr int kCvrpMaxRows = 64;
+#ifndef CO_CVRP_ROWS
+#define CO_CVRP_ROWS 64
+#endif
+#ifndef CO_CVRP_CPT
+#define CO_CVRP_CPT 2
+#endif
+constexpr int kCvrpCpt = CO_CVRP_CPT;
+constexpr int kCvrpMaxRows = CO_CVRP_ROWS;
 
 template <int THREADS>
 __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
