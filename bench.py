@@ -335,6 +335,7 @@ def main():
         # instance generation, timed separately (SURVEY.md 8d protocol; 8f rank 1)
         modes["slap_generate_b16384"] = bench_generate_slap(args.slap_batch, dev,
                                                             with_ref=(rank == 0 and world == 1))
+        modes["tsp_cvrp_generate"] = bench_generate_uniform(b, n, dev)
         annotate_modes(modes, n, world)
         out["modes"] = modes
 
@@ -506,6 +507,55 @@ def bench_generate_slap(b, dev, reps=3, with_ref=True):
         t0 = time.perf_counter()
         SLAPOracle(seed=1).generate([nb])
         out["reference_loop_ms_scaled"] = (time.perf_counter() - t0) / nb * b * 1e3
+    return out
+
+
+def bench_generate_uniform(b, n, dev, reps=5):
+    """TSP-100 / CVRP-100 instance generation (co_uniform_fill, Philox on the device) vs the
+    reference's host sampling (torch CPU RNG) + copy.  Device kernel timed with HIP events
+    (write-only: 4 B per element)."""
+    from rl4co_slap_amd import _native as nat
+    from rl4co_slap_amd.envs.cvrp import CVRPGenerator
+    from rl4co_slap_amd.envs.tsp import TSPGenerator
+
+    out = {}
+    for name, gd, gh in (("tsp", TSPGenerator(num_loc=n, device=dev), TSPGenerator(num_loc=n)),
+                         ("cvrp", CVRPGenerator(num_loc=n, device=dev), CVRPGenerator(num_loc=n))):
+        gd([b])
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            gd([b])
+        e1.record()
+        torch.cuda.synchronize(dev)
+        t_dev = e0.elapsed_time(e1) / 1e3 / reps
+        t0 = time.perf_counter()
+        gh([b]).to(dev)
+        torch.cuda.synchronize(dev)
+        t_host = time.perf_counter() - t0
+        out[name] = {"batch": b, "num_loc": n, "device_ms": t_dev * 1e3,
+                     "host_sample_plus_copy_ms": t_host * 1e3}
+    # the kernel alone: TSP locs fill, launches back to back on one stream
+    buf = torch.empty(b * n * 2, dtype=torch.float32, device=dev)
+    f = nat.bind("co_uniform_fill", nat.ptr(buf), buf.numel(), 0.0, 1.0, 1.0, 0, 1234, 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    f(s)
+    e0.record()
+    for _ in range(20):
+        f(s)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    t = e0.elapsed_time(e1) / 1e3 / 20
+    # write-only ceiling beside it: torch's fill of the same buffer
+    e0.record()
+    for _ in range(20):
+        buf.fill_(0.5)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    t_fill = e0.elapsed_time(e1) / 1e3 / 20
+    out["tsp"].update(kernel_us=t * 1e6, kernel_GBps_written=buf.numel() * 4 / t / 1e9,
+                      same_bytes_fill_us=t_fill * 1e6)
     return out
 
 

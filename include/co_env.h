@@ -324,6 +324,15 @@ int co_distance_matrix(int64_t batch, int64_t num_loc, const float* locs, float*
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 
+/* Device instance generation for throughput runs: the Uniform
+ * samplers of tsp/generator.py:51-60 and cvrp/generator.py:116-143 on a Philox-4x32-10
+ * stream (key = seed, block counter offset + i/4) instead of torch's CPU generator, so the
+ * values follow torch's f32 uniform grid and transform but not its stream (parity
+ * instances keep the host generators).  demand == 0: out[i] = low + u*(high-low);
+ * demand != 0: out[i] = ((int)(low + u*(high-low)) + 1) / capacity. */
+int co_uniform_fill(float* out, int64_t n, float low, float high, float capacity, int demand,
+                    uint64_t seed, uint64_t offset, void* stream);
+
 /* ------------------------------------------------ measurement utility (no reference
  * counterpart): dst[0:nbytes) = src[0:nbytes), one 16-byte load/store per thread over a
  * full grid -- the streaming ceiling the bench quotes beside each kernel's roofline.

@@ -177,6 +177,78 @@ extern "C" int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count,
   return launch_status();
 }
 
+// ------------------------------------------------------------------ instance generation
+// Device instance generator for throughput runs: the reference's
+// Uniform samplers (tsp/generator.py:51-60, cvrp/generator.py:116-143) on a counter-based
+// stream instead of torch's CPU Mersenne Twister.  One Philox-4x32-10 block (key = seed,
+// counter = (offset + i/4, 0)) gives elements 4*(i/4) .. 4*(i/4)+3; u = (x >> 8) * 2^-24
+// is torch's f32 uniform grid, out = low + u * (high - low) as Uniform.sample (two
+// roundings, no contraction); demand mode: out = ((int)(low + u * (high - low)) + 1) / cap.
+namespace {
+__device__ __forceinline__ uint4 philox4(uint64_t seed, uint64_t ctr) {
+  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0u, c3 = 0u;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0;
+    c1 = (uint32_t)p1;
+    c2 = n2;
+    c3 = (uint32_t)p0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+
+template <bool DEMAND>
+__device__ __forceinline__ float uniform_value(uint32_t x, float low, float range, float cap) {
+  const float u = (float)(x >> 8) * 0x1p-24f;
+  const float v = low + u * range;
+  return DEMAND ? (float)((int)v + 1) / cap : v;
+}
+
+template <bool DEMAND>
+__global__ __launch_bounds__(256) void uniform_fill_kernel(float* __restrict__ out, int64_t n,
+                                                           float low, float range, float cap,
+                                                           uint64_t seed, uint64_t offset) {
+  const int64_t nb = (n + 3) / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 x = philox4(seed, offset + (uint64_t)i);
+    const float4 v = make_float4(uniform_value<DEMAND>(x.x, low, range, cap),
+                                 uniform_value<DEMAND>(x.y, low, range, cap),
+                                 uniform_value<DEMAND>(x.z, low, range, cap),
+                                 uniform_value<DEMAND>(x.w, low, range, cap));
+    const int64_t e = 4 * i;
+    if (e + 4 <= n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+      *reinterpret_cast<float4*>(out + e) = v;
+    } else {
+      const float w[4] = {v.x, v.y, v.z, v.w};
+      for (int j = 0; j < 4 && e + j < n; ++j) out[e + j] = w[j];
+    }
+  }
+}
+}  // namespace
+
+extern "C" int co_uniform_fill(float* out, int64_t n, float low, float high, float capacity,
+                               int demand, uint64_t seed, uint64_t offset, void* stream) {
+  if (n < 0 || (n > 0 && !out) || !(high >= low) || (demand && !(capacity > 0.f)))
+    return CO_E_INVAL;
+  if (n == 0) return CO_OK;
+  const unsigned grid = grid_for((n + 3) / 4, 256, 256 * 64);
+  if (demand)
+    hipLaunchKernelGGL(uniform_fill_kernel<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       out, n, low, high - low, capacity, seed, offset);
+  else
+    hipLaunchKernelGGL(uniform_fill_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       out, n, low, high - low, 1.f, seed, offset);
+  return launch_status();
+}
+
 // ------------------------------------------------------------------ measurement probe
 namespace {
 // one 16-B unit per thread over a full grid (the float4-copy shape of the guide's 6.29 TB/s

@@ -4,7 +4,10 @@ from __future__ import annotations
 import abc
 from typing import Callable, Union
 
+import torch
 from torch.distributions import Exponential, Normal, Poisson, Uniform
+
+from .. import _native as nat
 
 
 class Generator(metaclass=abc.ABCMeta):
@@ -21,6 +24,28 @@ class Generator(metaclass=abc.ABCMeta):
     @abc.abstractmethod
     def _generate(self, batch_size, **kwargs):
         raise NotImplementedError
+
+
+def device_uniform(sampler, shape, device, capacity: float = None):
+    """Device instance generation for throughput runs (``co_uniform_fill``, SURVEY.md 8f
+    rank 1): ``sampler.sample(shape)`` for a scalar ``Uniform`` drawn on ``device`` from a
+    Philox stream.  Values follow torch's f32 uniform grid and ``low + u * (high - low)``;
+    the stream is not torch's CPU Mersenne Twister, so parity instances keep the host
+    samplers.  The Philox key is drawn from torch's global CPU generator, so
+    ``env.set_seed`` still makes the instances reproducible.  With ``capacity`` the
+    CVRP demand transform ``((int)v + 1) / capacity`` (``cvrp/generator.py:137-143``) is
+    applied in the same pass.  Returns ``None`` when ``sampler`` is not a scalar Uniform
+    (the caller then samples on the host)."""
+    if torch.device(device).type != "cuda" or not isinstance(sampler, Uniform) \
+            or sampler.low.numel() != 1 or sampler.high.numel() != 1:
+        return None
+    out = torch.empty(tuple(shape), dtype=torch.float32, device=device)
+    nat.require_device(out)
+    seed = int(torch.randint(0, 2 ** 62, (), dtype=torch.int64))
+    nat.call("co_uniform_fill", nat.ptr(out), out.numel(), float(sampler.low), float(sampler.high),
+             float(capacity) if capacity is not None else 1.0, int(capacity is not None), seed, 0,
+             nat.stream_of(out))
+    return out
 
 
 def get_sampler(val_name: str, distribution: Union[int, float, str, type, Callable], low: float = 0,

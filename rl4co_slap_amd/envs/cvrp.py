@@ -9,7 +9,7 @@ from torch.distributions import Uniform
 from .. import _native as nat
 from ..td import TensorDict
 from .base import RL4COEnvBase
-from .common import Generator, get_sampler
+from .common import Generator, device_uniform, get_sampler
 
 # cvrp/generator.py:15-30 (Kool et al. 2019, Hottung et al. 2022, Kim et al. 2023)
 CAPACITIES = {10: 20.0, 15: 25.0, 20: 30.0, 30: 33.0, 40: 37.0, 50: 40.0, 60: 43.0, 75: 45.0,
@@ -18,7 +18,8 @@ CAPACITIES = {10: 20.0, 15: 25.0, 20: 30.0, 30: 33.0, 40: 37.0, 50: 40.0, 60: 43
 
 class CVRPGenerator(Generator):
     """``cvrp/generator.py:33-143``: depot sampled with the customers when no depot
-    distribution is given; ``demand = (Uniform(min-1, max-1).int() + 1) / capacity``."""
+    distribution is given; ``demand = (Uniform(min-1, max-1).int() + 1) / capacity``.
+    With ``device="cuda"`` Uniform samplers draw on the GPU (``common.device_uniform``)."""
 
     def __init__(self, num_loc: int = 20, min_loc: float = 0.0, max_loc: float = 1.0,
                  loc_distribution: Union[int, float, str, type, Callable] = Uniform,
@@ -29,6 +30,7 @@ class CVRPGenerator(Generator):
         self.num_loc, self.min_loc, self.max_loc = num_loc, min_loc, max_loc
         self.min_demand, self.max_demand = min_demand, max_demand
         self.vehicle_capacity = vehicle_capacity
+        self.device = kwargs.get("device")
         self.loc_sampler = kwargs.get("loc_sampler") or get_sampler(
             "loc", loc_distribution, min_loc, max_loc, **kwargs)
         if kwargs.get("depot_sampler") is not None:
@@ -44,7 +46,25 @@ class CVRPGenerator(Generator):
             capacity = CAPACITIES[min(CAPACITIES, key=lambda x: abs(x - num_loc))]
         self.capacity = capacity
 
+    def _sample(self, sampler, shape, capacity=None):
+        out = device_uniform(sampler, shape, self.device, capacity) if self.device else None
+        if out is not None:
+            return out
+        out = sampler.sample(shape).to(self.device)
+        return out if capacity is None else (out.int() + 1).float() / capacity
+
     def _generate(self, batch_size) -> TensorDict:
+        if self.device:
+            if self.depot_sampler is not None:
+                depot = self._sample(self.depot_sampler, (*batch_size, 2))
+                locs = self._sample(self.loc_sampler, (*batch_size, self.num_loc, 2))
+            else:
+                locs = self._sample(self.loc_sampler, (*batch_size, self.num_loc + 1, 2))
+                depot, locs = locs[..., 0, :], locs[..., 1:, :]
+            demand = self._sample(self.demand_sampler, (*batch_size, self.num_loc), self.capacity)
+            capacity = torch.full((*batch_size, 1), self.capacity, device=demand.device)
+            return TensorDict({"locs": locs, "depot": depot, "demand": demand,
+                               "capacity": capacity}, batch_size=batch_size)
         if self.depot_sampler is not None:
             depot = self.depot_sampler.sample((*batch_size, 2))
             locs = self.loc_sampler.sample((*batch_size, self.num_loc, 2))

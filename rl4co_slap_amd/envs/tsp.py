@@ -9,23 +9,29 @@ from torch.distributions import Uniform
 from .. import _native as nat
 from ..td import TensorDict
 from .base import RL4COEnvBase
-from .common import Generator, get_sampler
+from .common import Generator, device_uniform, get_sampler
 
 
 class TSPGenerator(Generator):
     """``tsp/generator.py:14-60``: ``locs ~ Uniform(min_loc, max_loc)`` drawn from
-    torch's global CPU RNG (seeded by the env), shape ``[*B, num_loc, 2]``."""
+    torch's global CPU RNG (seeded by the env), shape ``[*B, num_loc, 2]``.  With
+    ``device="cuda"`` a Uniform sampler draws on the GPU instead (``common.device_uniform``:
+    same value grid, Philox stream keyed from the CPU RNG)."""
 
     def __init__(self, num_loc: int = 20, min_loc: float = 0.0, max_loc: float = 1.0,
                  init_sol_type: str = "random",
                  loc_distribution: Union[int, float, str, type, Callable] = Uniform, **kwargs):
         self.num_loc, self.min_loc, self.max_loc = num_loc, min_loc, max_loc
         self.init_sol_type = init_sol_type
+        self.device = kwargs.get("device")
         self.loc_sampler = kwargs.get("loc_sampler") or get_sampler(
             "loc", loc_distribution, min_loc, max_loc, **kwargs)
 
     def _generate(self, batch_size) -> TensorDict:
-        locs = self.loc_sampler.sample((*batch_size, self.num_loc, 2))
+        shape = (*batch_size, self.num_loc, 2)
+        locs = device_uniform(self.loc_sampler, shape, self.device) if self.device else None
+        if locs is None:
+            locs = self.loc_sampler.sample(shape)
         return TensorDict({"locs": locs}, batch_size=batch_size)
 
 

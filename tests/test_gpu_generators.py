@@ -29,3 +29,98 @@ def test_slap_device_generator_matches_host(dev, params, dist):
         assert devg[k].device.type == "cuda", k
         assert devg[k].dtype == host[k].dtype, k
         assert torch.equal(devg[k].cpu(), host[k]), k
+
+
+# ---------------------------------------------------------------- TSP / CVRP device generation
+from oracle.generate import uniform_fill as uniform_oracle  # noqa: E402
+from rl4co_slap_amd import _native as nat  # noqa: E402
+from rl4co_slap_amd.envs import CVRPEnv, TSPEnv  # noqa: E402
+from rl4co_slap_amd.envs.cvrp import CVRPGenerator  # noqa: E402
+from rl4co_slap_amd.envs.tsp import TSPGenerator  # noqa: E402
+
+
+def _fill(dev, n, low, high, seed, offset=0, capacity=None, storage_offset=0):
+    buf = torch.full((n + storage_offset,), -7.0, device=dev)
+    out = buf[storage_offset:]
+    nat.call("co_uniform_fill", nat.ptr(out), n, float(low), float(high),
+             float(capacity or 1.0), int(capacity is not None), seed, offset,
+             nat.stream_of(out))
+    torch.cuda.synchronize(dev)
+    if storage_offset:
+        assert (buf[:storage_offset] == -7.0).all()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("n,low,high,seed,offset,so", [
+    (1, 0.0, 1.0, 1, 0, 0), (5, 0.0, 1.0, 2, 0, 0), (4099, -2.0, 3.0, 2 ** 61 + 5, 17, 0),
+    (1 << 20, 0.0, 1.0, 99, 0, 0), ((1 << 20) + 3, 0.0, 1.0, 99, 0, 1), (6, 0.25, 0.25, 3, 0, 0)])
+def test_uniform_fill_matches_oracle(dev, n, low, high, seed, offset, so):
+    got = _fill(dev, n, low, high, seed, offset, storage_offset=so)
+    want = uniform_oracle(n, low, high, seed, offset)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("n,lo,hi,cap", [(37, 0.0, 9.0, 30.0), (100003, 0.0, 9.0, 50.0),
+                                         (4096, 2.0, 5.0, 1.0)])
+def test_uniform_fill_demand_matches_oracle(dev, n, lo, hi, cap):
+    got = _fill(dev, n, lo, hi, 11, capacity=cap)
+    assert np.array_equal(got, uniform_oracle(n, lo, hi, 11, capacity=cap))
+
+
+def test_uniform_fill_statistics_and_errors(dev):
+    v = _fill(dev, 1 << 22, 0.0, 1.0, 2024)
+    assert v.min() >= 0 and v.max() < 1
+    assert abs(v.mean() - 0.5) < 5 / np.sqrt(12 * v.size)
+    hist = np.bincount((v * 64).astype(int), minlength=64)
+    exp = v.size / 64
+    assert ((hist - exp) ** 2 / exp).sum() < 130  # chi-square, 63 dof (p << 1e-6 above)
+    out = torch.empty(4, device=dev)
+    with pytest.raises(RuntimeError):
+        nat.call("co_uniform_fill", nat.ptr(out), 4, 1.0, 0.0, 1.0, 0, 1, 0, nat.stream_of(out))
+    with pytest.raises(RuntimeError):
+        nat.call("co_uniform_fill", nat.ptr(out), 4, 0.0, 9.0, 0.0, 1, 1, 0, nat.stream_of(out))
+    nat.call("co_uniform_fill", None, 0, 0.0, 1.0, 1.0, 0, 1, 0, nat.stream_of(out))
+
+
+def test_tsp_device_generator(dev):
+    torch.manual_seed(3)
+    a = TSPGenerator(num_loc=50, device=dev)([64])
+    after = torch.rand(1).item()
+    torch.manual_seed(3)
+    b = TSPGenerator(num_loc=50, device=dev)([64])
+    assert torch.rand(1).item() == after  # one CPU draw (the Philox key) per sampler
+    assert a["locs"].device.type == "cuda" and a["locs"].shape == (64, 50, 2)
+    assert torch.equal(a["locs"], b["locs"])
+    torch.manual_seed(3)
+    seed = int(torch.randint(0, 2 ** 62, (), dtype=torch.int64))
+    want = uniform_oracle(64 * 50 * 2, 0.0, 1.0, seed).reshape(64, 50, 2)
+    assert np.array_equal(a["locs"].cpu().numpy(), want)
+    env = TSPEnv(generator_params={"num_loc": 50, "device": dev}, device=dev)
+    td = env.reset(batch_size=[32])
+    assert td["locs"].device.type == "cuda" and td["action_mask"].all()
+
+
+@pytest.mark.parametrize("depot_dist", [None, "uniform"])
+def test_cvrp_device_generator(dev, depot_dist):
+    n, b = 20, 48
+    torch.manual_seed(4)
+    td = CVRPGenerator(num_loc=n, device=dev, depot_distribution=depot_dist)([b])
+    torch.manual_seed(4)
+    g = CVRPGenerator(num_loc=n, device=dev, depot_distribution=depot_dist)
+    seeds = [int(torch.randint(0, 2 ** 62, (), dtype=torch.int64)) for _ in range(3)]
+    if depot_dist is None:
+        locs = uniform_oracle(b * (n + 1) * 2, 0.0, 1.0, seeds[0]).reshape(b, n + 1, 2)
+        depot, locs = locs[:, 0], locs[:, 1:]
+        dem_seed = seeds[1]
+    else:
+        depot = uniform_oracle(b * 2, 0.0, 1.0, seeds[0]).reshape(b, 2)
+        locs = uniform_oracle(b * n * 2, 0.0, 1.0, seeds[1]).reshape(b, n, 2)
+        dem_seed = seeds[2]
+    demand = uniform_oracle(b * n, 0.0, 9.0, dem_seed, capacity=g.capacity).reshape(b, n)
+    assert np.array_equal(td["depot"].cpu().numpy(), depot)
+    assert np.array_equal(td["locs"].cpu().numpy(), locs)
+    assert np.array_equal(td["demand"].cpu().numpy(), demand)
+    assert (td["capacity"] == g.capacity).all() and td["capacity"].device.type == "cuda"
+    env = CVRPEnv(generator=g, device=dev)
+    out = env.reset(td)
+    assert out["locs"].shape == (b, n + 1, 2) and out["action_mask"].shape == (b, n + 1)

@@ -147,3 +147,34 @@ def test_reference_shape_test(name):
     td = env.reset(batch_size=[2])
     r, _, _ = rollout(env, td, lambda t: torch.multinomial(t["action_mask"].float(), 1).squeeze(-1))
     assert r.shape == (2,)
+
+
+# Philox-4x32-10 known-answer vectors published with the Random123 library (kat_vectors):
+# (counter words, key words) -> output words.
+PHILOX_KAT = [
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+]
+
+
+@pytest.mark.parametrize("ctr,key,want", PHILOX_KAT)
+def test_philox_known_answers(ctr, key, want):
+    from oracle.generate import philox4x32_10
+
+    got = philox4x32_10(np.array([ctr], dtype=np.uint64), np.array([key], dtype=np.uint64))
+    assert tuple(int(v) for v in got[0]) == want
+
+
+def test_uniform_fill_oracle_grid_and_demand():
+    from oracle.generate import uniform_fill
+
+    v = uniform_fill(4099, 0.0, 1.0, seed=123)
+    assert v.dtype == np.float32 and v.shape == (4099,)
+    assert (v >= 0).all() and (v < 1).all()
+    assert np.array_equal(v * 2.0 ** 24, np.floor(v * 2.0 ** 24))
+    d = uniform_fill(20000, 0.0, 9.0, seed=7, capacity=40.0)
+    k = np.rint(d * 40.0).astype(int)
+    assert set(np.unique(k)) == set(range(1, 10))
+    assert np.array_equal(uniform_fill(10, 0, 1, seed=5, offset=1), uniform_fill(14, 0, 1, seed=5)[4:])

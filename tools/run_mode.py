@@ -1,6 +1,6 @@
 """Run one bench.py mode alone (for rocprofv3 kernel traces of a single path).
 
-    python tools/run_mode.py cvrp|slap|slap65k|pomo|tsp [--k K]
+    python tools/run_mode.py cvrp|slap|slap65k|pomo|tsp|gen [--k K]
 """
 import argparse
 import json
@@ -49,6 +49,8 @@ def main():
         cyc = itertools.cycle([e._bound for e in eps])
         wall, ev = bench.timed(lambda: next(cyc)(sh), a.k, 2, 1, dev)
         out = {"launch_us": ev / a.k * 1e6, "wall_us": wall / a.k * 1e6, "batches": n_rot}
+    elif a.mode == "gen":
+        out = bench.bench_generate_uniform(65536, 100, dev)
     else:
         raise SystemExit(f"unknown mode {a.mode}")
     print(json.dumps(out))
