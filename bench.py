@@ -482,7 +482,8 @@ def bench_cvrp(b, n, k, world, rank, dev):
 
 def bench_generate_slap(b, dev, reps=3, with_ref=True):
     """SLAP instance generation incl. the [B, 100, 100] dist_mat: co_slap_generate on the
-    device vs the host generator (vectorised) + copy; the oracle's restatement of the
+    device (freq/picklists from the host RNG streams; device_rng: from co_uniform_fill /
+    co_randint_fill too) vs the host generator (vectorised) + copy; the oracle's restatement of the
     reference's B x L Python loop is timed on a small sample and scaled per instance."""
     from rl4co_slap_amd.envs.slap import SLAPGenerator
 
@@ -498,8 +499,16 @@ def bench_generate_slap(b, dev, reps=3, with_ref=True):
     gh(b).to(dev)
     torch.cuda.synchronize(dev)
     t_host = time.perf_counter() - t0
-    out = {"device_ms": t_dev * 1e3, "host_vectorised_plus_copy_ms": t_host * 1e3,
-           "dist_mat_MB": b * 100 * 100 * 4 / 1e6}
+    gr = SLAPGenerator(device=dev, device_rng=True)
+    gr(b)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gr(b)
+    torch.cuda.synchronize(dev)
+    t_rng = (time.perf_counter() - t0) / reps
+    out = {"device_ms": t_dev * 1e3, "device_rng_ms": t_rng * 1e3,
+           "host_vectorised_plus_copy_ms": t_host * 1e3, "dist_mat_MB": b * 100 * 100 * 4 / 1e6}
     if with_ref:
         from oracle.envs import SLAPOracle
 

@@ -333,6 +333,12 @@ int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stre
 int co_uniform_fill(float* out, int64_t n, float low, float high, float capacity, int demand,
                     uint64_t seed, uint64_t offset, void* stream);
 
+/* Integers in [low, high) on the same Philox stream layout, for SLAP picklists in
+ * throughput runs (slap/generator.py:137-155 draws them with numpy's randint):
+ * out[i] = low + ((uint64)x_i * (high - low)) >> 32, 0 < high - low < 2^32. */
+int co_randint_fill(int64_t* out, int64_t n, int64_t low, int64_t high, uint64_t seed,
+                    uint64_t offset, void* stream);
+
 /* ------------------------------------------------ measurement utility (no reference
  * counterpart): dst[0:nbytes) = src[0:nbytes), one 16-byte load/store per thread over a
  * full grid -- the streaming ceiling the bench quotes beside each kernel's roofline.

@@ -32,16 +32,26 @@ def philox4x32_10(ctr, key):
     return np.stack(c, axis=-1)
 
 
-def uniform_fill(n, low, high, seed, offset=0, capacity=None):
-    """Element ``i`` of ``co_uniform_fill``: word ``i % 4`` of the block at counter
-    ``offset + i // 4`` (counter words 0/1 = its low/high halves, 2/3 = 0), key = seed."""
+def _words(n, seed, offset):
     nb = (n + 3) // 4
     blk = np.arange(nb, dtype=np.uint64) + np.uint64(offset)
     ctr = np.zeros((nb, 4), dtype=np.uint64)
     ctr[:, 0] = blk & np.uint64(MASK)
     ctr[:, 1] = blk >> np.uint64(32)
     key = np.array([seed & MASK, seed >> 32], dtype=np.uint64)[None, :]
-    x = philox4x32_10(ctr, key).reshape(-1)[:n]
+    return philox4x32_10(ctr, key).reshape(-1)[:n]
+
+
+def randint_fill(n, low, high, seed, offset=0):
+    """``co_randint_fill``: ``low + (x * (high - low)) >> 32`` on the same stream layout."""
+    x = _words(n, seed, offset)
+    return np.int64(low) + ((x * np.uint64(high - low)) >> np.uint64(32)).astype(np.int64)
+
+
+def uniform_fill(n, low, high, seed, offset=0, capacity=None):
+    """Element ``i`` of ``co_uniform_fill``: word ``i % 4`` of the block at counter
+    ``offset + i // 4`` (counter words 0/1 = its low/high halves, 2/3 = 0), key = seed."""
+    x = _words(n, seed, offset)
     u = (x >> np.uint64(8)).astype(np.float32) * np.float32(2.0 ** -24)
     v = np.float32(low) + u * (np.float32(high) - np.float32(low))
     if capacity is None:

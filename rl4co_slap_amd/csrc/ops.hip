@@ -232,7 +232,39 @@ __global__ __launch_bounds__(256) void uniform_fill_kernel(float* __restrict__ o
     }
   }
 }
+// integers in [low, low + range): low + (x * range) >> 32 (multiply-shift; the bias is
+// below range / 2^32, e.g. 5e-9 for range 20)
+__global__ __launch_bounds__(256) void randint_fill_kernel(int64_t* __restrict__ out, int64_t n,
+                                                           int64_t low, uint32_t range,
+                                                           uint64_t seed, uint64_t offset) {
+  const int64_t nb = (n + 3) / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 x = philox4(seed, offset + (uint64_t)i);
+    const int64_t w[4] = {low + (int64_t)(((uint64_t)x.x * range) >> 32),
+                          low + (int64_t)(((uint64_t)x.y * range) >> 32),
+                          low + (int64_t)(((uint64_t)x.z * range) >> 32),
+                          low + (int64_t)(((uint64_t)x.w * range) >> 32)};
+    const int64_t e = 4 * i;
+    if (e + 4 <= n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+      *reinterpret_cast<longlong2*>(out + e) = make_longlong2(w[0], w[1]);
+      *reinterpret_cast<longlong2*>(out + e + 2) = make_longlong2(w[2], w[3]);
+    } else {
+      for (int j = 0; j < 4 && e + j < n; ++j) out[e + j] = w[j];
+    }
+  }
+}
 }  // namespace
+
+extern "C" int co_randint_fill(int64_t* out, int64_t n, int64_t low, int64_t high, uint64_t seed,
+                               uint64_t offset, void* stream) {
+  if (n < 0 || (n > 0 && !out) || !(high > low) || high - low > (int64_t)0xffffffffLL)
+    return CO_E_INVAL;
+  if (n == 0) return CO_OK;
+  hipLaunchKernelGGL(randint_fill_kernel, dim3(grid_for((n + 3) / 4, 256, 256 * 64)), dim3(256),
+                     0, (hipStream_t)stream, out, n, low, (uint32_t)(high - low), seed, offset);
+  return launch_status();
+}
 
 extern "C" int co_uniform_fill(float* out, int64_t n, float low, float high, float capacity,
                                int demand, uint64_t seed, uint64_t offset, void* stream) {

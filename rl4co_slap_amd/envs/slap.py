@@ -8,7 +8,7 @@ import torch
 from .. import _native as nat
 from ..td import TensorDict
 from .base import RL4COEnvBase
-from .common import Generator
+from .common import Generator, device_uniform
 
 
 class SLAPGenerator(Generator):
@@ -27,7 +27,7 @@ class SLAPGenerator(Generator):
     def __init__(self, n_products: int = 20, n_aisles: int = 10, n_locs: int = 10,
                  inter_loc_dist: float = 1, inter_aisle_dist: float = 2.4, min_freq: int = 1,
                  max_freq: int = 20, max_orders: int = 20, max_products_in_order: int = 5,
-                 materialize_dist_mat: bool = True, device=None):
+                 materialize_dist_mat: bool = True, device=None, device_rng: bool = False):
         self.n_products, self.n_aisles, self.n_locs = n_products, n_aisles, n_locs
         self.max_orders, self.max_products_in_order = max_orders, max_products_in_order
         self.inter_loc_dist, self.inter_aisle_dist = inter_loc_dist, inter_aisle_dist
@@ -38,6 +38,10 @@ class SLAPGenerator(Generator):
         # matrices, assignment) are written by co_slap_generate on the device; freq and the
         # picklists keep the host RNG streams and are copied (1.3 + 13 MB at B = 16,384)
         self.device = None if device is None else torch.device(device)
+        # device_rng (throughput runs only): freq and picklists drawn on the device too
+        # (co_uniform_fill / co_randint_fill, Philox keyed by one torch CPU draw) -- the
+        # same distributions, not the reference's torch/numpy streams
+        self.device_rng = device_rng
 
     @staticmethod
     def _get_distance_matrix(locs: torch.Tensor):
@@ -74,9 +78,17 @@ class SLAPGenerator(Generator):
     def _generate_device(self, batch_size) -> TensorDict:
         dev = self.device
         b, L, P = batch_size[0], self.n_aisles * self.n_locs, self.n_products
-        freq = self.freq_sampler.sample((*batch_size, P, 1))  # same draw order as the host path
-        picklist = torch.from_numpy(np.random.randint(
-            0, P, size=(b, self.max_orders, self.max_products_in_order)).astype(np.int64))
+        if self.device_rng:
+            freq = device_uniform(self.freq_sampler, (*batch_size, P, 1), dev)
+            picklist = torch.empty((b, self.max_orders, self.max_products_in_order),
+                                   dtype=torch.int64, device=dev)
+            seed = int(torch.randint(0, 2 ** 62, (), dtype=torch.int64))
+            nat.call("co_randint_fill", nat.ptr(picklist), picklist.numel(), 0, P, seed, 0,
+                     nat.stream_of(picklist))
+        else:
+            freq = self.freq_sampler.sample((*batch_size, P, 1))  # host path's draw order
+            picklist = torch.from_numpy(np.random.randint(
+                0, P, size=(b, self.max_orders, self.max_products_in_order)).astype(np.int64))
         locs = torch.empty((b, L, 2), dtype=torch.float32, device=dev)
         depot = torch.empty((b, L), dtype=torch.float32, device=dev)
         assign = torch.empty((b, P), dtype=torch.int32, device=dev)

@@ -34,7 +34,7 @@ def test_slap_device_generator_matches_host(dev, params, dist):
 # ---------------------------------------------------------------- TSP / CVRP device generation
 from oracle.generate import uniform_fill as uniform_oracle  # noqa: E402
 from rl4co_slap_amd import _native as nat  # noqa: E402
-from rl4co_slap_amd.envs import CVRPEnv, TSPEnv  # noqa: E402
+from rl4co_slap_amd.envs import CVRPEnv, SLAPEnv, TSPEnv  # noqa: E402
 from rl4co_slap_amd.envs.cvrp import CVRPGenerator  # noqa: E402
 from rl4co_slap_amd.envs.tsp import TSPGenerator  # noqa: E402
 
@@ -124,3 +124,42 @@ def test_cvrp_device_generator(dev, depot_dist):
     env = CVRPEnv(generator=g, device=dev)
     out = env.reset(td)
     assert out["locs"].shape == (b, n + 1, 2) and out["action_mask"].shape == (b, n + 1)
+
+
+def test_randint_fill_matches_oracle(dev):
+    from oracle.generate import randint_fill
+
+    for n, lo, hi, seed, off in [(1, 0, 20, 1, 0), (7, 0, 20, 9, 3), (20 * 5 * 1001, 0, 20, 77, 0),
+                                 (33, -5, 2 ** 32 - 6, 2 ** 60 + 1, 0)]:
+        out = torch.full((n,), -99, dtype=torch.int64, device=dev)
+        nat.call("co_randint_fill", nat.ptr(out), n, lo, hi, seed, off, nat.stream_of(out))
+        got = out.cpu().numpy()
+        assert np.array_equal(got, randint_fill(n, lo, hi, seed, off))
+        assert got.min() >= lo and got.max() < hi
+    out = torch.empty(4, dtype=torch.int64, device=dev)
+    for lo, hi in [(3, 3), (0, 2 ** 32 + 1)]:
+        with pytest.raises(RuntimeError):
+            nat.call("co_randint_fill", nat.ptr(out), 4, lo, hi, 1, 0, nat.stream_of(out))
+
+
+def test_slap_device_rng_generator(dev):
+    from oracle.generate import randint_fill
+
+    b = 300
+    torch.manual_seed(8)
+    np.random.seed(8)
+    g = SLAPGenerator(device=dev, device_rng=True)
+    td = g(b)
+    assert np.random.rand() == np.random.RandomState(8).rand()  # numpy's stream untouched
+    torch.manual_seed(8)
+    seeds = [int(torch.randint(0, 2 ** 62, (), dtype=torch.int64)) for _ in range(2)]
+    freq = uniform_oracle(b * 20, 1.0, 20.0, seeds[0]).reshape(b, 20, 1)
+    pick = randint_fill(b * 20 * 5, 0, 20, seeds[1]).reshape(b, 20, 5)
+    assert np.array_equal(td["freq"].cpu().numpy(), freq)
+    assert np.array_equal(td["picklist"].cpu().numpy(), pick)
+    host = SLAPGenerator()(b)
+    for k in ("locs", "depot_loc_dist", "dist_mat", "assignment"):
+        assert torch.equal(td[k].cpu(), host[k]), k
+    env = SLAPEnv(generator=g, device=dev)
+    out = env.reset(batch_size=[b])
+    assert out["action_mask"].shape == (b, 100)
