@@ -160,8 +160,13 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
     if (c < nchunks) v[k] = tile_load(vsrc, c << 4, nbytes, true);
   }
   // demand tile -> LDS by LDS-DMA; the helper's vmcnt(0) + barrier also covers the loads above
+#if CO_CVRP_CUT & 1  // timing diagnostic only (tools/diag_cvrp_step.py): no demand tile
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+#else
   stage_bytes_lds(reinterpret_cast<const unsigned char*>(demand + row0 * N), rows * N * 4,
                   reinterpret_cast<unsigned char*>(s_dem));
+#endif
   if (tid < rows) {  // cvrp/env.py:79-85
     const bool bad = a_raw < 0 || a_raw > N;
     if (bad) set_status(status, CO_ST_INDEX_RANGE);
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
   __syncthreads();
 
   // Each chunk spans at most two rows (NC >= 17): r0 from byte 0, r1 from byte `split`.
-  // Per byte only selects (no branches); each chunk leaves (sum, any-feasible) of both row
+  // No branches per byte (selects and word-wide byte arithmetic); each chunk leaves (sum, any-feasible) of both row
   // parts in LDS and one thread per row adds its ~NC/16 parts after the barrier.
   uint4 m[kCvrpCpt];
   uint8_t* vdst = vis_out + row0 * NC;
@@ -191,11 +196,14 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
     const float u0 = s_u[r0], cp0 = s_cap[r0];
     const float u1 = has1 ? s_u[r1] : 0.f, cp1 = has1 ? s_cap[r1] : 0.f;
     const int dbase = off - r0 - 1;  // s_dem index of byte j: dbase + j (row r0), one less (r1)
-    union {
-      uint4 v;
-      uint8_t b[16];
-    } uv, um;
-    uv.v = v[k];
+    uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#if CO_CVRP_CUT & 2  // timing diagnostic only: no per-byte update
+    s_part[2 * ch] = 0;
+    s_part[2 * ch + 1] = 0;
+    tile_store(vdst, off, nbytes, true, v[k]);
+    m[k] = v[k];
+    continue;
+#endif
     // all 16 demand reads issued before any use (a short-circuit `||` would put each
     // behind a branch and an lgkmcnt(0) wait)
     float dm[16];
@@ -204,26 +212,46 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
       int di = dbase + j - (j >= split ? 1 : 0);
       dm[j] = s_dem[di < 0 ? 0 : di];
     }
-    int cnt0 = 0, cnt1 = 0, feas0 = 0, feas1 = 0;
+    // Per byte only the capacity test (f32 add + compare, as the reference) sets a flag bit;
+    // the rest is word-wide (SWAR) on the chunk's four u32 words: r0 / r1 byte masks from
+    // `split`, the action byte of each row set to 1, the nonzero test, byte sums by
+    // v_sad_u8, the customer mask and its any-feasible tests.
+    const int ja0 = (act0 >= c0 && act0 - c0 < split) ? act0 - c0 : -1;  // byte of r0's action
+    const int ja1 = (act1 >= 0 && split + act1 < 16) ? split + act1 : -1;
+    int cnt0 = 0, cnt1 = 0;
+    uint32_t f0 = 0u, f1 = 0u, um_w[4];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const bool sec = j >= split;
-      const int c = sec ? j - split : c0 + j;
-      uint8_t x = uv.b[j];
-      x = (c == (sec ? act1 : act0)) ? (uint8_t)1 : x;
-      uv.b[j] = x;
-      const bool masked = (x != 0) | (dm[j] + (sec ? u1 : u0) > (sec ? cp1 : cp0));
-      const int mk = (c > 0 && off + j < nbytes && !masked) ? 1 : 0;
-      um.b[j] = (uint8_t)mk;
-      cnt0 += sec ? 0 : x;
-      cnt1 += sec ? x : 0;
-      feas0 |= sec ? 0 : mk;
-      feas1 |= sec ? mk : 0;
+    for (int q = 0; q < 4; ++q) {
+      const int lo = split - 4 * q;  // bytes of this word that belong to r0
+      const uint32_t m0 = lo >= 4 ? 0xffffffffu : lo <= 0 ? 0u : (1u << (8 * lo)) - 1u;
+      uint32_t x = w[q];
+      if ((ja0 >> 2) == q) x = (x & ~(0xffu << (8 * (ja0 & 3)))) | (1u << (8 * (ja0 & 3)));
+      if ((ja1 >> 2) == q) x = (x & ~(0xffu << (8 * (ja1 & 3)))) | (1u << (8 * (ja1 & 3)));
+      w[q] = x;
+      uint32_t over = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = 4 * q + e;
+        const bool sec = j >= split;
+        over |= (dm[j] + (sec ? u1 : u0) > (sec ? cp1 : cp0)) ? (0x80u << (8 * e)) : 0u;
+      }
+      const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+      uint32_t mk = (~(nz | over) & 0x80808080u) >> 7;
+      // depot bytes (column 0: byte 0 when r0 starts here, byte `split` for r1) are left 0
+      // here and patched after the row sums; they take no part in any-feasible
+      if (q == 0 && c0 == 0) mk &= ~0xffu;
+      if ((split >> 2) == q && split < 16) mk &= ~(0xffu << (8 * (split & 3)));
+      cnt0 = __builtin_amdgcn_sad_u8(x & m0, 0u, cnt0);
+      cnt1 = __builtin_amdgcn_sad_u8(x & ~m0, 0u, cnt1);
+      f0 |= mk & m0;
+      f1 |= mk & ~m0;
+      um_w[q] = mk;
     }
+    const int feas0 = f0 != 0u, feas1 = f1 != 0u;
     s_part[2 * ch] = cnt0 | (feas0 << 16);
     s_part[2 * ch + 1] = cnt1 | (feas1 << 16);
-    tile_store(vdst, off, nbytes, true, uv.v);
-    m[k] = um.v;
+    tile_store(vdst, off, nbytes, true, make_uint4(w[0], w[1], w[2], w[3]));
+    m[k] = make_uint4(um_w[0], um_w[1], um_w[2], um_w[3]);
   }
   __syncthreads();
   if (tid < rows) {  // row sums over the row's chunk parts
