@@ -132,7 +132,8 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
     const float* __restrict__ vcap, const uint8_t* vis_in, uint8_t* vis_out,
     int64_t* __restrict__ cur_out, uint8_t* __restrict__ done, uint8_t* __restrict__ reward,
     uint8_t* __restrict__ mask, int32_t* status, int32_t* not_done) {
-  extern __shared__ float s_dem[];  // [R, N]
+  extern __shared__ float s_dem_raw[];  // 4 pad floats, then [R, N]
+  float* const s_dem = s_dem_raw + 4;
   __shared__ int s_act[kCvrpMaxRows];
   __shared__ float s_u[kCvrpMaxRows], s_cap[kCvrpMaxRows];
   __shared__ int s_cnt[kCvrpMaxRows], s_feas[kCvrpMaxRows];
@@ -206,12 +207,14 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
 #endif
     // all 16 demand reads issued before any use (a short-circuit `||` would put each
     // behind a branch and an lgkmcnt(0) wait)
-    float dm[16];
+    // 17 consecutive floats from one base (static offsets, no per-read address math): byte
+    // j of r0 takes D[j + 1], of r1 D[j]; the first tile's base is -2 (pad floats, unused)
+    float D[17], dm[16];
+    const float* dp = s_dem + dbase - 1;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      int di = dbase + j - (j >= split ? 1 : 0);
-      dm[j] = s_dem[di < 0 ? 0 : di];
-    }
+    for (int t = 0; t < 17; ++t) D[t] = dp[t];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dm[j] = j >= split ? D[j] : D[j + 1];
     // Per byte only the capacity test (f32 add + compare, as the reference) sets a flag bit;
     // the rest is word-wide (SWAR) on the chunk's four u32 words: r0 / r1 byte masks from
     // `split`, the action byte of each row set to 1, the nonzero test, byte sums by
@@ -497,10 +500,10 @@ extern "C" int co_cvrp_step(int64_t B, int64_t N, const int64_t* action, const f
                         15) == 0;
   int R = (int)((256 * kCvrpCpt * 16) / NC);
   R = (R > kCvrpMaxRows ? kCvrpMaxRows : R) & ~15;
-  if (N >= 16 && aligned && R >= 16 && (size_t)R * N * sizeof(float) <= 64 * 1024) {
+  if (N >= 16 && aligned && R >= 16 && (size_t)R * N * sizeof(float) + 16 <= 64 * 1024) {
     const unsigned grid = (unsigned)((B + R - 1) / R);
     hipLaunchKernelGGL(cvrp_step_tile_kernel<256>, dim3(grid), dim3(256),
-                       (size_t)R * N * sizeof(float), (hipStream_t)stream, B, (int)N, R, action,
+                       (size_t)R * N * sizeof(float) + 16, (hipStream_t)stream, B, (int)N, R, action,
                        demand, used_in, used_out, vcap, vis_in, vis_out, cur_out, done, reward,
                        mask, status, not_done);
     return launch_status();
