@@ -15,7 +15,9 @@ import sys
 
 rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+path = os.path.join(root, "profiles", f"{rnd}_pmc_traffic.json")
 out = {"note": __doc__.strip(), "kernels": {}}
+new = {}
 for d in sorted(glob.glob(os.path.join(root, "gpurun_out/pmc/*.*_SIZE"))):
     target, counter = os.path.basename(d).rsplit(".", 1)
     f = os.path.join(d, "run_counter_collection.csv")
@@ -29,14 +31,19 @@ for d in sorted(glob.glob(os.path.join(root, "gpurun_out/pmc/*.*_SIZE"))):
         short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         agg[short].append(float(r["Counter_Value"]))
     for k, v in agg.items():
-        e = out["kernels"].setdefault(f"{target}:{k}", {"target": target, "kernel": k})
+        e = new.setdefault(f"{target}:{k}", {"target": target, "kernel": k})
         e[counter + "_KiB_mean"] = sum(v) / len(v)
         e["dispatches_" + counter] = len(v)
-for k, e in out["kernels"].items():
+for k, e in new.items():
     if "FETCH_SIZE_KiB_mean" in e and "WRITE_SIZE_KiB_mean" in e:
         e["hbm_read_bytes"] = 2 * e["FETCH_SIZE_KiB_mean"] * 1024
         e["hbm_write_bytes"] = e["WRITE_SIZE_KiB_mean"] * 1024
         e["hbm_bytes_per_launch"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
-path = os.path.join(root, "profiles", f"{rnd}_pmc_traffic.json")
+# targets measured in this pass replace their earlier entries; other targets are kept
+if os.path.exists(path):
+    old = json.load(open(path))["kernels"]
+    done = {e["target"] for e in new.values()}
+    out["kernels"] = {k: e for k, e in old.items() if e.get("target") not in done}
+out["kernels"].update(new)
 json.dump(out, open(path, "w"), indent=1)
-print(json.dumps(out["kernels"], indent=1))
+print(json.dumps(new, indent=1))
