@@ -394,8 +394,10 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
   extern __shared__ uint32_t s_mem[];
   const int w = threadIdx.x >> 6, lane = lane_id();
   const int words = (N + 32) >> 5;  // bits for values 0..N
-  uint32_t* bits = s_mem + w * (words + T);
+  uint32_t* bits = s_mem + w * (words + 4 * T);
   float* dseq = reinterpret_cast<float*>(bits + words);
+  int* starts = reinterpret_cast<int*>(dseq + T);  // route (segment) start steps
+  float* sval = dseq + 2 * T;                       // [2][T] route start values (ping-pong)
   for (int64_t b = (int64_t)blockIdx.x * WAVES + w; b < B; b += (int64_t)gridDim.x * WAVES) {
     const int64_t* arow = actions + b * sb;
     const float2* lrow = locs + b * (int64_t)(N + 1);
@@ -406,31 +408,43 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
     }
     const float cap = check ? vcap[b] : 0.f;
     double acc = 0.0;
-    bool bad = false, range = false;
-    int nonzero = 0;
+    bool bad = false, range = false, start_here = false;
+    int nonzero = 0, nseg = 0;
     const int M = T + 1;
-    for (int m = lane; m < M; m += 64) {
-      const int64_t a_from = (m == 0) ? 0 : arow[(int64_t)(m - 1) * st];
-      const int64_t a_to = (m + 1 == M) ? 0 : arow[(int64_t)m * st];
-      if (a_from < 0 || a_from > N || a_to < 0 || a_to > N) {
-        range = true;
-      } else {
-        const float2 p = lrow[a_from], q = lrow[a_to];
-        acc += (double)edge_len(p.x, p.y, q.x, q.y);
-      }
-      if (check && m < T) {
-        const int64_t a = a_to;  // = actions[m]
-        if (a < 0 || a > N) {
-          bad = true;
-          dseq[m] = 0.f;
+    for (int base = 0; base < M; base += 64) {  // wave-uniform trip count (ballot below)
+      const int m = base + lane;
+      if (m < M) {
+        const int64_t a_from = (m == 0) ? 0 : arow[(int64_t)(m - 1) * st];
+        const int64_t a_to = (m + 1 == M) ? 0 : arow[(int64_t)m * st];
+        if (check && m < T && a_from == 0) start_here = true;  // step 0 or right after a depot
+        if (a_from < 0 || a_from > N || a_to < 0 || a_to > N) {
+          range = true;
         } else {
-          if (a != 0) {
-            ++nonzero;
-            const uint32_t bit = 1u << (a & 31);
-            if (atomicOr(&bits[a >> 5], bit) & bit) bad = true;
-          }
-          dseq[m] = (a == 0) ? -cap : demand[b * (int64_t)N + a - 1];
+          const float2 p = lrow[a_from], q = lrow[a_to];
+          acc += (double)edge_len(p.x, p.y, q.x, q.y);
         }
+        if (check && m < T) {
+          const int64_t a = a_to;  // = actions[m]
+          if (a < 0 || a > N) {
+            bad = true;
+            dseq[m] = 0.f;
+          } else {
+            if (a != 0) {
+              ++nonzero;
+              const uint32_t bit = 1u << (a & 31);
+              if (atomicOr(&bits[a >> 5], bit) & bit) bad = true;
+            }
+            dseq[m] = (a == 0) ? -cap : demand[b * (int64_t)N + a - 1];
+          }
+        }
+      }
+      if (check) {  // route starts, in step order
+        const uint64_t bal = __ballot(start_here);
+        if (start_here)
+          starts[nseg + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = m;
+        nseg += __popcll(bal);
+        start_here = false;
       }
     }
     acc = wave_sum(acc);
@@ -441,21 +455,62 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
       const bool invalid = __any(bad) || nonzero != N;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        if (invalid) {
-          set_status(status, CO_ST_INVALID_TOUR);
-        } else {
-          // cvrp/env.py:181-190, sequential f32 scan
-          const float lim = cap + 1e-5f;
-          float used = 0.f;
-          bool over = false;
-          for (int t = 0; t < T; ++t) {
-            used += dseq[t];
-            if (used < 0.f) used = 0.f;
-            if (!(used <= lim)) over = true;
+      if (invalid) {
+        if (lane == 0) set_status(status, CO_ST_INVALID_TOUR);
+      } else {
+        // cvrp/env.py:181-190: used = max(used + d_t, 0), over if !(used <= cap + 1e-5), a
+        // sequential f32 scan.  Split at the routes (step 0 / a depot's next step through
+        // the next depot): route k starts from the value route k-1 ends with, exactly 0
+        // unless that route ended in (cap, cap + 1e-5] (f32 sums of demands often land a
+        // hair above cap).  Each lane scans its routes -- the reference's f32 operations in
+        // its order -- from the current start values; a route whose end differs from its
+        // successor's start value updates it and the routes are scanned again, until no
+        // start changes (one repeat per chain of residual routes).  Every pass's values are
+        // <= the sequential ones (f32 add and max are monotone), so an overflow seen in any
+        // pass is one the sequential scan sees, and the last pass is the sequential scan.
+        const float lim = cap + 1e-5f;
+        bool over = false;
+        float* cur_v = sval;
+        float* nxt_v = sval + T;
+        for (int k = lane; k < nseg; k += 64) cur_v[k] = nxt_v[k] = 0.f;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#if !CO_CVRP_RCUT
+        // an overflow is final (stop); a NaN demand overflows; at most nseg passes
+        for (int pass = 0, again = 1; again && pass < nseg; ++pass) {
+          bool changed = false;
+          for (int k = lane; k < nseg; k += 64) {
+            const int t0 = starts[k], t1 = k + 1 < nseg ? starts[k + 1] : T;
+            float used = cur_v[k];
+            // 8 steps per block, their LDS reads issued together; steps past the route add
+            // +0.f (used >= 0 stays bit-identical up to the sign of a zero, which no
+            // comparison sees)
+            for (int t = t0; t < t1; t += 8) {
+              float d[8];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) d[i] = t + i < t1 ? dseq[t + i] : 0.f;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                used += d[i];
+                if (used < 0.f) used = 0.f;
+                if (!(used <= lim)) over = true;
+              }
+            }
+            if (k + 1 < nseg) {
+              nxt_v[k + 1] = used;
+              changed |= used != cur_v[k + 1];
+            }
           }
-          if (over) set_status(status, CO_ST_OVER_CAPACITY);
+          again = __any(changed) && !__any(over);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          float* tmp = cur_v;
+          cur_v = nxt_v;
+          nxt_v = tmp;
         }
+#endif
+        over = __any(over);
+        if (over && lane == 0) set_status(status, CO_ST_OVER_CAPACITY);
       }
     }
   }
@@ -534,7 +589,7 @@ extern "C" int co_cvrp_reward(int64_t B, int64_t N, int64_t T, const float* locs
   if (!locs || !actions || !reward) return CO_E_INVAL;
   if (check && (!demand || !vcap || !status)) return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
-  const size_t per_wave = check ? (size_t)((N + 32) / 32 + T) * 4 : 0;
+  const size_t per_wave = check ? (size_t)((N + 32) / 32 + 4 * T) * 4 : 0;
   // step-major actions ([T, B] rows): 16 consecutive instances per workgroup, so each
   // 128-B line of an action row is consumed on one CU (4 per workgroup spread a line over
   // 4 XCDs' L2s: 160 MB read per launch at B = 32,768, T = 112, vs ~70 MB algorithmic)

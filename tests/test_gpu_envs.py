@@ -299,3 +299,69 @@ def test_empty_batch(dev):
     td["action"] = torch.zeros(0, dtype=torch.int64, device=dev)
     td = env.step(td)["next"]
     assert td["action_mask"].shape == (0, 10)
+
+
+def _cvrp_reward_status(dev, depot_locs, actions, demand, step_major):
+    """co_cvrp_reward with check=1 on [b, T] actions; returns (reward, status bits)."""
+    from rl4co_slap_amd import _native as nat
+
+    b, T = actions.shape
+    n = demand.shape[1]
+    acts = (actions.t() if step_major else actions).contiguous().to(dev)
+    sb, st = (1, b) if step_major else (T, 1)
+    lf, dm = depot_locs.contiguous().to(dev), demand.contiguous().to(dev)
+    vcap = torch.ones(b, device=dev)
+    reward = torch.empty(b, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    nat.call("co_cvrp_reward", b, n, T, nat.ptr(lf), nat.ptr(acts), sb, st, nat.ptr(dm),
+             nat.ptr(vcap), 1, nat.ptr(reward), nat.ptr(status), nat.stream_of(acts))
+    return reward.cpu(), int(status.item())
+
+
+def _oracle_over(demand, actions):
+    from oracle.envs import CVRPOracle
+
+    td = TD({"demand": demand, "vehicle_capacity": torch.ones(demand.shape[0], 1)}, [demand.shape[0]])
+    try:
+        CVRPOracle.check_solution_validity(td, actions)
+    except AssertionError as e:
+        return "capacity" in str(e)
+    return False
+
+
+@pytest.mark.parametrize("step_major", [False, True])
+def test_cvrp_reward_capacity_scan_routes(dev, step_major):
+    """The route-parallel capacity scan equals the reference's sequential scan per row,
+    including routes that end in (cap, cap + 1e-5] and leave a residual for the next one
+    (the lane-0 sequential repeat) -- rows checked one launch each (status is batch-wide)."""
+    g = torch.Generator().manual_seed(17)
+    rows = []
+    # residual 3.8e-6 after route 1; route 2 overflows only with it / fits even with it
+    for tail, want in (([0.5, 0.500008], True), ([0.5, 0.5], False)):
+        dm = torch.tensor([[0.5, 0.5000038] + tail])
+        rows.append((dm, torch.tensor([[1, 2, 0, 3, 4, 0, 0]]), want))
+    for r in range(40):
+        n = int(torch.randint(5, 40, (1,), generator=g))
+        dm = (torch.randint(1, 10, (1, n), generator=g).float() / 10.0)
+        perm = torch.randperm(n, generator=g) + 1
+        acts, used = [], 0.0
+        for c in perm.tolist():  # greedy routes; some rows deliberately overfill one route
+            if used + dm[0, c - 1].item() > 1.0 and not (r % 5 == 0 and len(acts) < 4):
+                acts.append(0)
+                used = 0.0
+            acts.append(c)
+            used += dm[0, c - 1].item()
+        acts += [0] * int(torch.randint(1, 4, (1,), generator=g))
+        rows.append((dm, torch.tensor([acts]), None))
+    n_over = 0
+    for dm, acts, want in rows:
+        n = dm.shape[1]
+        locs = torch.rand(1, n + 1, 2, generator=g)
+        _, st = _cvrp_reward_status(dev, locs, acts, dm, step_major)
+        over = _oracle_over(dm, acts)
+        if want is not None:
+            assert over == want
+        assert bool(st & 2) == over, (dm, acts)
+        assert not st & 1
+        n_over += over
+    assert 3 <= n_over < len(rows)
