@@ -411,21 +411,36 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
     bool bad = false, range = false, start_here = false;
     int nonzero = 0, nseg = 0;
     const int M = T + 1;
+    // lane m loads action m and its coordinates once; the edge's start node comes from
+    // lane m-1 (shuffle) or, for lane 0, from the previous block's lane 63 (depot at m = 0)
+    int a_carry = 0;
+    float px_carry = lrow[0].x, py_carry = lrow[0].y;
     for (int base = 0; base < M; base += 64) {  // wave-uniform trip count (ballot below)
       const int m = base + lane;
+      const int64_t a_to = (m < T) ? arow[(int64_t)m * st] : 0;  // m == T: back to the depot
+      const bool ok_to = a_to >= 0 && a_to <= N;
+      const int a32 = ok_to ? (int)a_to : -1;
+      const float2 q = lrow[ok_to && m < M ? a32 : 0];
+      int a_from = __shfl_up(a32, 1, 64);
+      float px = __shfl_up(q.x, 1, 64), py = __shfl_up(q.y, 1, 64);
+      if (lane == 0) {
+        a_from = a_carry;
+        px = px_carry;
+        py = py_carry;
+      }
+      a_carry = __shfl(a32, 63, 64);
+      px_carry = __shfl(q.x, 63, 64);
+      py_carry = __shfl(q.y, 63, 64);
       if (m < M) {
-        const int64_t a_from = (m == 0) ? 0 : arow[(int64_t)(m - 1) * st];
-        const int64_t a_to = (m + 1 == M) ? 0 : arow[(int64_t)m * st];
         if (check && m < T && a_from == 0) start_here = true;  // step 0 or right after a depot
-        if (a_from < 0 || a_from > N || a_to < 0 || a_to > N) {
+        if (a_from < 0 || !ok_to) {
           range = true;
         } else {
-          const float2 p = lrow[a_from], q = lrow[a_to];
-          acc += (double)edge_len(p.x, p.y, q.x, q.y);
+          acc += (double)edge_len(px, py, q.x, q.y);
         }
         if (check && m < T) {
           const int64_t a = a_to;  // = actions[m]
-          if (a < 0 || a > N) {
+          if (!ok_to) {
             bad = true;
             dseq[m] = 0.f;
           } else {
