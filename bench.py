@@ -330,6 +330,9 @@ def main():
         # POMO TSP-100 (config 5): 1,024 instances x 100 starts per GPU, decode-fused steps
         # on HBM-resident logits, shared baseline + RCCL all-gather of per-instance results
         modes["pomo_tsp100"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev)
+        # the same with the opt-in CO_DECODE_FAST math (not bit-exact; reported separately)
+        modes["pomo_tsp100_fast_math"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev,
+                                                    fast_math=True)
         # CVRP-100 (config 3), nearest-feasible policy: fused episode and stepwise loop
         modes.update(bench_cvrp(32768, 100, k, world, rank, dev))
         # instance generation, timed separately (SURVEY.md 8d protocol; 8f rank 1)
@@ -363,6 +366,7 @@ def annotate_modes(modes, n, world):
         "slap_fused_random_b65536": lambda m: 2354 / 20,
         "slap_stepwise_graph": lambda m: 234 + 1684 / 20,
         "pomo_tsp100": lambda m: 6 * n + 54,
+        "pomo_tsp100_fast_math": lambda m: 6 * n + 54,
         "cvrp_fused_nearest": lambda m: (8 + 12 * n + 8 * m["episode_steps"] + 10 * (n + 1) + 25)
         / m["episode_steps"],
         "cvrp_stepwise_graph": lambda m: 7 * n + 33 + (16 * m["episode_steps"] + 12)
@@ -568,7 +572,7 @@ def bench_generate_uniform(b, n, dev, reps=5):
     return out
 
 
-def bench_pomo(b, n, k, world, rank, dev):
+def bench_pomo(b, n, k, world, rank, dev, fast_math=False):
     from rl4co_slap_amd.rollout.pomo import POMOEpisode, global_metrics
 
     torch.manual_seed(1234 + rank)
@@ -576,7 +580,7 @@ def bench_pomo(b, n, k, world, rank, dev):
     e = b * n
     g = torch.Generator(device=dev).manual_seed(99 + rank)
     logits = torch.randn((n - 1, e, n), generator=g, device=dev)  # policy-network stand-in
-    ep = POMOEpisode(locs, logits, tanh_clipping=10.0).capture()
+    ep = POMOEpisode(locs, logits, tanh_clipping=10.0, fast_math=fast_math).capture()
 
     def run():
         ep.replay()
@@ -591,6 +595,8 @@ def bench_pomo(b, n, k, world, rank, dev):
     return {"value": world * e * n * k / t, "ms_per_episode": t / k * 1e3,
             "instances_per_gpu": b, "starts": n, "envs_per_gpu": e,
             "bytes_per_env_step_decode_fused": 6 * n + 54,
+            "decode_math": "fast (CO_DECODE_FAST, opt-in, not bit-exact)" if fast_math
+            else "exact (ATen log_softmax bits, correctly rounded tanh)",
             "allgather_ms": t_ag * 1e3, "global_instances": m["instances"],
             "loss": float(m["loss"]), "max_reward_mean": float(m["max_reward_mean"])}
 

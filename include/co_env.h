@@ -164,11 +164,17 @@ int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t* flag, voi
 #define CO_DECODE_GREEDY 0
 #define CO_DECODE_SAMPLING 1
 #define CO_DECODE_EVALUATE 2
+/* mode flag (OR-ed into `mode`), opt-in: hardware v_exp tanh / exp and lane-order sums.
+ * Without it the step is ATen-exact: logp bit-identical to F.log_softmax of the processed
+ * logits (SLEEF expf/logf and vec::map_reduce_all's 16-lane order), tanh correctly
+ * rounded; with it logp is within ~1e-6 and greedy picks may differ on near-ties. */
+#define CO_DECODE_FAST 0x100
 
 /* DecodingStrategy.step (rl4co/utils/decoding.py:141-191,327-399,489-499):
  * x = logits[b*logits_stride + c]; tanh clip (tanh_clipping > 0); masked
  * (mask != NULL and mask[b*n+c] == 0) -> -inf; x /= temperature;
- * logp = (x - max) - log(sum(exp(x - max)));
+ * logp = (x - max) - log(sum(exp(x - max))) (ATen's CPU evaluation, bit-exact; see
+ * CO_DECODE_FAST);
  * greedy: first argmax of logp (torch tie-break); sampling: inverse CDF of
  * exp(logp) with a Philox draw keyed by (seed, offset, b); evaluate: action_in.
  * action_out[b], logp_sel[b] = logp[b, action]; logprobs_full (nullable)

@@ -23,11 +23,19 @@ def top_p_filter(logits, top_p):  # decoding.py:120-138
     return logits.masked_fill(remove, float("-inf"))
 
 
+def tanh_cr(x):
+    """tanh rounded once from f64: what the device decode step evaluates (torch.tanh on
+    CPU is MKL VML's, within one ulp of it; see rl4co_slap_amd/csrc/co_math.hpp)."""
+    return torch.tanh(x.double()).float()
+
+
 def process_logits(logits, mask=None, temperature=1.0, tanh_clipping=0.0, mask_logits=True,
-                   top_k=0, top_p=0.0):
-    """``decoding.py:141-191`` (ties of the top-p sort in index order: stable sort)."""
+                   top_k=0, top_p=0.0, tanh=torch.tanh):
+    """``decoding.py:141-191`` (ties of the top-p sort in index order: stable sort).
+    ``tanh`` defaults to the reference's ``torch.tanh``; tests pass ``tanh_cr`` to separate
+    the tanh implementation from the rest of the math."""
     if tanh_clipping > 0:
-        logits = torch.tanh(logits) * tanh_clipping
+        logits = tanh(logits) * tanh_clipping
     if mask_logits:
         assert mask is not None, "mask must be provided if mask_logits is True"
         logits = logits.clone()
@@ -71,7 +79,8 @@ class Decoding:
     evaluate, with multistart (``pre_decoder_hook`` ``:265-313``)."""
 
     def __init__(self, kind="greedy", temperature=1.0, tanh_clipping=0.0, mask_logits=True,
-                 multistart=False, num_starts=None, store_all_logp=False):
+                 multistart=False, num_starts=None, store_all_logp=False, tanh=torch.tanh):
+        self.tanh = tanh  # tests only: odec.tanh_cr to match the device tanh
         self.kind = kind.replace("multistart_", "")
         self.multistart = multistart or kind.startswith("multistart")
         self.temperature, self.tanh_clipping, self.mask_logits = temperature, tanh_clipping, mask_logits
@@ -98,7 +107,8 @@ class Decoding:
 
     def step(self, logits, mask, td, action=None):  # decoding.py:327-369
         m = mask if self.mask_logits else None
-        logp = process_logits(logits, m, self.temperature, self.tanh_clipping, self.mask_logits)
+        logp = process_logits(logits, m, self.temperature, self.tanh_clipping, self.mask_logits,
+                              tanh=self.tanh)
         if self.kind == "greedy":
             sel = greedy(logp, m)
         elif self.kind == "sampling":

@@ -67,6 +67,7 @@ ST_OVER_CAPACITY = 2
 ST_INFEASIBLE = 4
 ST_INDEX_RANGE = 8
 ST_TRUNCATED = 16
+DECODE_FAST = 0x100  # CO_DECODE_FAST mode flag (opt-in fast math; not bit-exact)
 
 _lock = threading.Lock()
 _lib = None

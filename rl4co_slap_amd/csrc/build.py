@@ -19,7 +19,7 @@ OUT_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(OUT_DIR, "libco_env.so")
 SOURCES = ["tsp.hip", "cvrp.hip", "slap.hip", "ops.hip", "decode.hip", "rollout.hip",
            "nearest.hip"]
-HEADERS = ["co_common.hpp", "co_tile.hpp"]
+HEADERS = ["co_common.hpp", "co_tile.hpp", "co_math.hpp"]
 ARCH = "gfx950"
 
 

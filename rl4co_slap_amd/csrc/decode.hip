@@ -8,6 +8,7 @@
 // same association as ATen's CPU kernel: logp = (x - max) - log(sum(exp(x - max))),
 // so greedy ties resolve exactly like torch.argmax (first index).
 #include "co_common.hpp"
+#include "co_math.hpp"
 
 using namespace co;
 
@@ -32,33 +33,50 @@ using namespace co;
 #define CO_DECODE_UNR 1
 #endif
 __device__ __forceinline__ float co_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-// tanh(x) = 1 - 2 / (e^{2x} + 1) on v_exp / v_rcp (abs error ~1e-7, exact +-1 saturation)
+// CO_DECODE_FAST (opt-in, mode flag): tanh(x) = 1 - 2 / (e^{2x} + 1) on v_exp / v_rcp (abs
+// error ~1e-7, exact +-1 saturation), the softmax exps on v_exp_f32 (<= 2 ulp) summed in
+// lane order -- log-probabilities within ~1e-6 of the reference, greedy picks exact only
+// where the top two are further apart than that
 __device__ __forceinline__ float co_tanh_fast(float x) {
   const float e = co_exp2(x * 2.8853900817779268f);  // e^{2x}
   return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f);
 }
 __device__ __forceinline__ float co_exp_fast(float x) { return co_exp2(x * 1.4426950408889634f); }
 
-#ifndef CO_FAST_EXP
-#define CO_FAST_EXP 1  // hardware v_exp_f32 in the softmax sums (<= 2 ulp; logp parity is 1e-5)
-#endif
-#if CO_FAST_EXP
-#define CO_EXPF co_exp_fast
-#else
-#define CO_EXPF expf
-#endif
-#ifndef CO_GREEDY_FAST
-#define CO_GREEDY_FAST 1  // greedy rows on GreedyRow (first index at the max logp)
-#endif
-#ifndef CO_FAST_TANH
-#define CO_FAST_TANH 1
-#endif
-#if CO_FAST_TANH
-// against ~25 instructions for the libm tanhf
-__device__ __forceinline__ float co_tanhf(float x) { return co_tanh_fast(x); }
-#else
-__device__ __forceinline__ float co_tanhf(float x) { return tanhf(x); }
-#endif
+// OPT template flags of the row engines: bit 0 tanh clipping, bit 1 temperature != 1,
+// bit 2 the fast math above (default: ATen-exact, co_math.hpp)
+constexpr int kOptClip = 1, kOptTemp = 2, kOptFast = 4;
+
+template <int OPT>
+__device__ __forceinline__ float clip_tanh(float x) {
+  return (OPT & kOptFast) ? co_tanh_fast(x) : tanh_cr(x);
+}
+
+// exp-sum of a row (x already shifted by the row max; out-of-row slots excluded) and its
+// log: ATen's order and SLEEF math (exact) or v_exp + lane-order butterfly (fast)
+template <int RL, int EPL, int OPT>
+__device__ __forceinline__ float row_log_sum_exp(const float (&d)[EPL], int N, int sl,
+                                                 float* lds_row) {
+  const int c0 = sl * EPL;
+  float e[EPL];
+  if (OPT & kOptFast) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) s += c0 + k < N ? co_exp_fast(d[k]) : 0.f;
+    return logf(grp_sum<RL>(s));
+  }
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) e[k] = c0 + k < N ? aten_expf(d[k]) : 0.f;
+  return aten_logf(aten_row_sum<RL, EPL>(e, N, sl, lds_row));
+}
+
+// LDS scratch of the exact sums: one RL*EPL-float row per lane group = 64*EPL floats per
+// wave; kernels of 256 threads (4 waves) declare it as `__shared__ float[4 * 64 * EPL]`
+// (unused, and dropped by the compiler, on the fast path)
+template <int RL, int EPL>
+__device__ __forceinline__ float* group_scratch(float* lds, int grp) {
+  return lds + (threadIdx.x >> 6) * (64 * EPL) + grp * (RL * EPL);
+}
 
 namespace {
 
@@ -135,9 +153,10 @@ struct DecodeRow {  // OPT: clip / temperature flags as in GreedyRow::softmax_sh
   __device__ __forceinline__ void run(bool valid, int N, const float* lrow, const uint8_t* mrow,
                                       float clip, float temp, int mode, int64_t a_in,
                                       uint64_t seed, uint64_t offset, int64_t row, int sl,
-                                      int grp, int top_k = 0, double top_p = 0.0) {
+                                      int grp, float* lds_row, int top_k = 0,
+                                      double top_p = 0.0) {
     load(valid, N, lrow, mrow, sl);
-    compute(valid, N, clip, temp, mode, a_in, seed, offset, row, sl, grp, top_k, top_p);
+    compute(valid, N, clip, temp, mode, a_in, seed, offset, row, sl, grp, lds_row, top_k, top_p);
   }
 
   // decoding.py:112-117 modify_logits_for_top_k_filtering on x (the processed logits):
@@ -216,8 +235,8 @@ struct DecodeRow {  // OPT: clip / temperature flags as in GreedyRow::softmax_sh
   // the math on data already `load`ed (callers overlap several rows' loads)
   __device__ __forceinline__ void compute(bool valid, int N, float clip, float temp, int mode,
                                           int64_t a_in, uint64_t seed, uint64_t offset,
-                                          int64_t row, int sl, int grp, int top_k = 0,
-                                          double top_p = 0.0) {
+                                          int64_t row, int sl, int grp, float* lds_row,
+                                          int top_k = 0, double top_p = 0.0) {
     const float NEG_INF = -__builtin_inff();
     const int c0 = sl * EPL;
     float m = NEG_INF;
@@ -226,9 +245,9 @@ struct DecodeRow {  // OPT: clip / temperature flags as in GreedyRow::softmax_sh
       float v = NEG_INF;
       if (valid && c0 + k < N) {
         v = x[k];
-        if (OPT & 1) v = co_tanhf(v) * clip;
+        if (OPT & kOptClip) v = clip_tanh<OPT>(v) * clip;
         if (!mk[k]) v = NEG_INF;
-        if (OPT & 2) v = v / temp;  // x / 1 == x exactly: skip the IEEE divide
+        if (OPT & kOptTemp) v = v / temp;  // x / 1 == x exactly: skip the IEEE divide
         m = fmaxf(m, v);
       }
       x[k] = v;
@@ -236,14 +255,11 @@ struct DecodeRow {  // OPT: clip / temperature flags as in GreedyRow::softmax_sh
     m = grp_max<RL>(m);
     if (top_k > 0 && top_k < N) filter_top_k(N, top_k, sl);
     if (top_p > 0.0 && top_p < 1.0) filter_top_p(valid, N, top_p, m, sl, grp);
-    float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < EPL; ++k)
-      if (valid && c0 + k < N) s += CO_EXPF(x[k] - m);
-    s = grp_sum<RL>(s);
-    const float L = logf(s);
+    for (int k = 0; k < EPL; ++k) x[k] = x[k] - m;
+    const float L = row_log_sum_exp<RL, EPL, OPT>(x, N, sl, lds_row);
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) x[k] = (x[k] - m) - L;  // ATen association
+    for (int k = 0; k < EPL; ++k) x[k] = x[k] - L;  // ATen association: (x - m) - L
     sel = 0;
     if (mode == CO_DECODE_GREEDY) {
       float bv = NEG_INF;
@@ -403,28 +419,23 @@ struct GreedyRow {
   // OPT bit 0: tanh clipping, bit 1: temperature != 1 (template flags: as runtime
   // conditions the compiler evaluates both arms per element and selects)
   template <int OPT>
-  __device__ __forceinline__ float softmax_shift(float clip, float temp) {
+  __device__ __forceinline__ float softmax_shift(float clip, float temp, int N, int sl,
+                                                 float* lds_row) {
     const float NEG_INF = -__builtin_inff();
     float m = NEG_INF;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
       float t = v[k];
-      if (OPT & 1) t = co_tanhf(t) * clip;
-      if (OPT & 2) t = t / temp;
+      if (OPT & kOptClip) t = clip_tanh<OPT>(t) * clip;
+      if (OPT & kOptTemp) t = t / temp;
       t = allowed(k) ? t : NEG_INF;
       v[k] = t;
       m = fmaxf(m, t);
     }
     m = grp_max<RL>(m);
-    float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const float d = v[k] - m;
-      v[k] = d;
-      s += CO_EXPF(d);
-    }
-    s = grp_sum<RL>(s);
-    return logf(s);
+    for (int k = 0; k < EPL; ++k) v[k] = v[k] - m;
+    return row_log_sum_exp<RL, EPL, OPT>(v, N, sl, lds_row);
   }
 
   // greedy action of the row (valid on every lane of the group) and its logp
@@ -444,6 +455,7 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
     const uint8_t* __restrict__ mask, float clip, float temp, int64_t* __restrict__ action_out,
     float* __restrict__ logp_sel, float* __restrict__ full, int32_t* status) {
   constexpr int RPW = 64 / RL;
+  __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -453,7 +465,7 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
     const int64_t r = valid ? row : 0;
     GreedyRow<RL, EPL, VW> g;
     g.load(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, c0);
-    const float L = g.template softmax_shift<OPT>(clip, temp);
+    const float L = g.template softmax_shift<OPT>(clip, temp, N, sl, group_scratch<RL, EPL>(lds, grp));
     float lp;
     const int sel = g.select(L, c0, lp);
     if (!valid) continue;
@@ -477,6 +489,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
                                                      uint64_t offset, int32_t* status, int top_k,
                                                      double top_p) {
   constexpr int RPW = 64 / RL;
+  __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -487,7 +500,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
     const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
     DecodeRow<RL, EPL, VEC, OPT> d;
     d.run(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, clip, temp,
-          mode, a_in, seed, offset, row, sl, grp, top_k, top_p);
+          mode, a_in, seed, offset, row, sl, grp, group_scratch<RL, EPL>(lds, grp), top_k, top_p);
     if (!valid) continue;
     if (full) {
 #pragma unroll
@@ -519,6 +532,7 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
     uint8_t* __restrict__ done, uint8_t* __restrict__ step_reward, float* __restrict__ ll_accum,
     int32_t* status) {
   constexpr int RPW = 64 / RL;
+  __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -546,7 +560,7 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
       const bool valid = vv[u];
       const int64_t r = rr[u], a_in = ain[u];
       d[u].compute(valid, N, clip, temp, mode, a_in, seed, offset, base + u * RPW + grp, sl,
-                   grp);
+                   grp, group_scratch<RL, EPL>(lds, grp));
       bool any_left = false;
       uint8_t* orow = mask_out + r * (int64_t)N;
       const int c0 = sl * EPL;
@@ -597,6 +611,7 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     int64_t* __restrict__ first_out, int take_first, uint8_t* __restrict__ done,
     uint8_t* __restrict__ step_reward, float* __restrict__ ll_accum, int32_t* status) {
   constexpr int RPW = 64 / RL;
+  __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -614,7 +629,7 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     }
     GreedyRow<RL, EPL, VW> g;
     g.load(valid, N, logits + r * lstride, mask_in + r * (int64_t)N, c0);
-    const float L = g.template softmax_shift<OPT>(clip, temp);
+    const float L = g.template softmax_shift<OPT>(clip, temp, N, sl, group_scratch<RL, EPL>(lds, grp));
     float lp;
     const int sel = g.select(L, c0, lp);
     const bool feas0 = g.allowed(0);
@@ -651,23 +666,26 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
   else if (N <= 1024) LAUNCH(64, 16, V);                     \
   else LAUNCH(64, 32, V)
 
-// the uniform clip / temperature options as the OPT template flags of the greedy kernels
-#define CO_OPT_DISPATCH(LAUNCH, KERNEL, ...)                       \
-  do {                                                             \
-    const int opt_ = (clip > 0.f ? 1 : 0) | (temp != 1.f ? 2 : 0); \
-    if (opt_ == 0) {                                               \
-      constexpr int OPT = 0;                                       \
-      LAUNCH(KERNEL, __VA_ARGS__);                                 \
-    } else if (opt_ == 1) {                                        \
-      constexpr int OPT = 1;                                       \
-      LAUNCH(KERNEL, __VA_ARGS__);                                 \
-    } else if (opt_ == 2) {                                        \
-      constexpr int OPT = 2;                                       \
-      LAUNCH(KERNEL, __VA_ARGS__);                                 \
-    } else {                                                       \
-      constexpr int OPT = 3;                                       \
-      LAUNCH(KERNEL, __VA_ARGS__);                                 \
-    }                                                              \
+// the uniform clip / temperature / fast-math options as the OPT template flags
+#define CO_OPT_CASE(V, LAUNCH, KERNEL, ...) \
+  case V: {                                 \
+    constexpr int OPT = V;                  \
+    LAUNCH(KERNEL, __VA_ARGS__);            \
+    break;                                  \
+  }
+#define CO_OPT_DISPATCH(LAUNCH, KERNEL, ...)                                            \
+  do {                                                                                  \
+    switch ((clip > 0.f ? kOptClip : 0) | (temp != 1.f ? kOptTemp : 0) |                \
+            (fast ? kOptFast : 0)) {                                                    \
+      CO_OPT_CASE(0, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+      CO_OPT_CASE(1, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+      CO_OPT_CASE(2, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+      CO_OPT_CASE(3, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+      CO_OPT_CASE(4, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+      CO_OPT_CASE(5, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+      CO_OPT_CASE(6, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+      CO_OPT_CASE(7, LAUNCH, KERNEL, __VA_ARGS__)                                       \
+    }                                                                                   \
   } while (0)
 
 inline unsigned decode_grid(int64_t B, int N, int unr = 1) {
@@ -701,6 +719,8 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
                                  uint64_t offset, int32_t* status, void* stream) {
   if (B < 0 || N <= 0 || N > 64 * 32 || top_k < 0 || top_p < 0.0 || top_p > 1.0)
     return CO_E_INVAL;
+  const bool fast = (mode & CO_DECODE_FAST) != 0;
+  mode &= ~CO_DECODE_FAST;
   if (mode < 0 || mode > 2) return CO_E_MODE;
   if (B == 0) return CO_OK;
   if (!logits || !action_out) return CO_E_INVAL;
@@ -708,7 +728,7 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
   const dim3 grid(decode_grid(B, (int)N)), block(256);
   hipStream_t s = (hipStream_t)stream;
   const bool filtered = (top_k > 0 && top_k < N) || (top_p > 0.0 && top_p < 1.0);
-  if (CO_GREEDY_FAST && mode == CO_DECODE_GREEDY && !filtered) {
+  if (mode == CO_DECODE_GREEDY && !filtered) {
 #define CO_GREEDY(RL, EPL, V)                                                                  \
   CO_OPT_DISPATCH(hipLaunchKernelGGL, (decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>),  \
                   grid, block, 0, s, B, (int)N, logits, lstride, mask, clip, temp, action_out,  \
@@ -752,6 +772,8 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
                                   uint8_t* done, uint8_t* step_reward, float* ll_accum,
                                   int32_t* status, void* stream) {
   if (B < 0 || N <= 0 || N > 64 * 32) return CO_E_INVAL;
+  const bool fast = (mode & CO_DECODE_FAST) != 0;
+  mode &= ~CO_DECODE_FAST;
   if (mode < 0 || mode > 2 || first_mode < 0 || first_mode > 1) return CO_E_MODE;
   if (B == 0) return CO_OK;
   if (!logits || !mask_in || !action_out || !mask_out || !i_in || !i_out || !first_out ||
@@ -759,7 +781,7 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
       (mode == CO_DECODE_EVALUATE && !action_in))
     return CO_E_INVAL;
   hipStream_t s = (hipStream_t)stream;
-  if (CO_GREEDY_FAST && mode == CO_DECODE_GREEDY) {
+  if (mode == CO_DECODE_GREEDY) {
     const dim3 grid(decode_grid(B, (int)N)), block(256);
 #define CO_TDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH(hipLaunchKernelGGL,                                                          \

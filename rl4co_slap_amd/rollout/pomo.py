@@ -33,7 +33,7 @@ from .engine import _GraphEpisode
 
 class POMOEpisode(_GraphEpisode):
     def __init__(self, locs: torch.Tensor, logits: torch.Tensor, num_starts: int = None,
-                 tanh_clipping: float = 10.0, check: bool = True):
+                 tanh_clipping: float = 10.0, check: bool = True, fast_math: bool = False):
         super().__init__(locs.device)
         b, n, _ = locs.shape
         s = n if num_starts is None else num_starts
@@ -42,6 +42,8 @@ class POMOEpisode(_GraphEpisode):
         d = locs.device
         self.b, self.n, self.s, self.e = b, n, s, e
         self.clip, self.check = float(tanh_clipping), check
+        # fast_math: CO_DECODE_FAST (opt-in; log-probs within ~1e-6, not bit-exact)
+        self.mode = nat.DECODE_FAST if fast_math else 0
         self.locs, self.logits = locs.contiguous(), logits.contiguous()
         self.acts = torch.empty((n, e), dtype=torch.int64, device=d)
         self.acts[0] = torch.arange(s, device=d).repeat_interleave(b) % n  # ops.py:150-154
@@ -75,7 +77,8 @@ class POMOEpisode(_GraphEpisode):
             src, dst = t & 1, (t + 1) & 1
             lg = self.logits[t - 1]
             nat.call("co_tsp_decode_step", e, n, nat.ptr(lg), lg.stride(0), nat.ptr(self.mask[src]),
-                     self.clip, 1.0, 0, None, nat.ptr(self.acts[t]), nat.ptr(self.logp[t]), 0, t,
+                     self.clip, 1.0, self.mode, None, nat.ptr(self.acts[t]), nat.ptr(self.logp[t]),
+                     0, t,
                      nat.ptr(self.mask[dst]), nat.ptr(self.i[src]), nat.ptr(self.i[dst]),
                      nat.ptr(self.first[src]), nat.ptr(self.first[dst]), 0, nat.ptr(self.done),
                      nat.ptr(self.step_reward), nat.ptr(self.ll), nat.ptr(self.status), st)

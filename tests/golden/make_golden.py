@@ -103,8 +103,11 @@ def decode(b, n, clip):
     mask[torch.arange(b), torch.randint(0, n, (b,), generator=g)] = True
     logp = odec.process_logits(logits, mask, temperature=1.0, tanh_clipping=clip)
     act = logp.argmax(-1)
-    return {"logits": logits.numpy(), "mask": mask.numpy(), "clip": np.float32(clip),
-            "action": act.numpy(), "logp_sel": logp.gather(1, act[:, None]).squeeze(1).numpy()}
+    out = {"logits": logits.numpy(), "mask": mask.numpy(), "clip": np.float32(clip),
+           "action": act.numpy(), "logp_sel": logp.gather(1, act[:, None]).squeeze(1).numpy()}
+    if clip > 0:  # the oracle's post-clip logits (decoding.py:172-173, torch.tanh on the CPU)
+        out["logits_clipped"] = (torch.tanh(logits) * clip).numpy()
+    return out
 
 
 def pomo(b, n):
@@ -126,7 +129,9 @@ def pomo(b, n):
     return {"locs": locs.numpy(), "logits": logits.numpy(), "actions": out["actions"].numpy(),
             "reward": out["reward"].numpy(), "log_likelihood": out["log_likelihood"].numpy(),
             "bl_val": ref["bl_val"].squeeze(1).numpy(), "max_reward": ref["max_reward"].numpy(),
-            "loss": np.float32(ref["loss"])}
+            "loss": np.float32(ref["loss"]),
+            # the post-clip logits the oracle decoded (torch.tanh on the CPU, x 10)
+            "logits_clipped": (torch.tanh(logits) * 10.0).numpy()}
 
 
 def build_all():

@@ -27,14 +27,14 @@ for B, N in [(102400, 100), (65536, 100), (102400, 20), (102400, 50), (16384, 20
     sr = torch.empty_like(done)
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream().cuda_stream
-    for clip in ((float(os.environ.get("DIAG_CLIP", "0")),) if os.environ.get("DIAG_QUICK") else (0.0, 10.0)):
+    for clip, fast in [(c, f) for c in ((0.0, 10.0)) for f in (0, nat.DECODE_FAST)]:
         for name in ("decode", "tsp_decode"):
             def run():
                 if name == "decode":
-                    nat.call("co_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, 0,
+                    nat.call("co_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, fast,
                              None, nat.ptr(out_a), nat.ptr(lp), None, 0, 0, nat.ptr(st), s)
                 else:
-                    nat.call("co_tsp_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, 0,
+                    nat.call("co_tsp_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, fast,
                              None, nat.ptr(out_a), nat.ptr(lp), 0, 0, nat.ptr(m2), nat.ptr(i0),
                              nat.ptr(i1), nat.ptr(f0), nat.ptr(f1), 0, nat.ptr(done), nat.ptr(sr),
                              None, nat.ptr(st), s)
@@ -60,4 +60,5 @@ for B, N in [(102400, 100), (65536, 100), (102400, 20), (102400, 50), (16384, 20
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / 50
             byts = B * (5 * N + 16) if name == "decode" else B * (6 * N + 54)
-            print(f"B={B} N={N} clip={clip} {name}: {us:.1f} us  {byts / us / 1e3:.0f} GB/s")
+            print(f"B={B} N={N} clip={clip} fast={bool(fast)} {name}: {us:.1f} us  "
+                  f"{byts / us / 1e3:.0f} GB/s", flush=True)
