@@ -45,13 +45,42 @@ def parse():
     ap.add_argument("--slap-batch", type=int, default=16384)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-modes", action="store_true", help="headline only")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU plumbing check: gloo ranks, the CPU oracle episode as the step "
+                         "(no GPU, no HIP library); rehearses --gpus N launches in a container")
     return ap.parse_args()
 
 
-def setup_dist():
+def launch_ranks(args):
+    """--gpus N > 1 without a torch.distributed launcher around us: start one rank per GPU
+    as children of this process (which has not touched the GPU) through
+    torch.distributed.run on 127.0.0.1 and exit with its status."""
+    import socket
+    import subprocess
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank "
+                         f"per GPU (torch.distributed.run --nproc-per-node {args.gpus}) or drop "
+                         f"the launcher and let bench.py start them")
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return world, rank, torch.device("cpu")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -61,6 +90,11 @@ def setup_dist():
 def barrier(world):
     if world > 1:
         dist.barrier()
+
+
+def sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
 
 
 def max_over_ranks(x, world, dev):
@@ -152,6 +186,30 @@ def copy_probe(traffic_bytes, dev, k):
 def cpu_threads():
     # the box's CPU share (OMP_NUM_THREADS is set to it on the GPU pool), not the whole host
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+
+
+def host_cpu():
+    """The host the CPU baseline ran on (BASELINE.md 2 asks for the CPU model and cores)."""
+    model, cores, sockets = None, set(), set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys = v
+                sockets.add(v)
+            elif k == "core id":
+                core = v
+                cores.add((phys, core))
+    except OSError:
+        pass
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(),
+            "physical_cores": len(cores) or None, "sockets": len(sockets) or None,
+            "threads_used": cpu_threads(),
+            "aten_capability": torch.backends.cpu.get_cpu_capability()}
 
 
 def cpu_baseline_tsp(locs, acts, episodes=3):
@@ -251,7 +309,11 @@ def pmc_traffic(target, kernel_prefix):
 
 def main():
     args = parse()
-    world, rank, dev = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world, rank, dev = setup_dist(args)
+    if args.dry_run:
+        return dry_run(args, world, rank, dev)
     from rl4co_slap_amd import _native
     from rl4co_slap_amd.rollout.engine import TSPFusedEpisode, TSPStepwiseEpisode
 
@@ -344,9 +406,55 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_tsp(locs_cpu, acts_cpu)
+        out["cpu_baseline"]["host"] = host_cpu()
         if not args.no_modes:
             out["cpu_baseline_slap"] = cpu_baseline_slap()
             out["cpu_baseline_cvrp"] = cpu_baseline_cvrp()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run(args, world, rank, dev):
+    """CPU rehearsal of the launch / reduction / JSON path (no GPU, no HIP library): each
+    gloo rank runs the oracle's TSP teacher episode on its own instance shard as the
+    step, ranks are timed with the same barrier + max-over-ranks protocol, and the POMO
+    all-gather runs on the oracle's per-instance baseline values."""
+    from oracle.envs import TSPOracle
+    from oracle.rollout import rollout
+    from oracle.td import TD
+    from rl4co_slap_amd.rollout.pomo import global_metrics
+
+    b, n = min(args.batch, 512), min(args.num_loc, 20)
+    locs, acts = tsp_inputs(b, n, rank)
+    env = TSPOracle(num_loc=n, seed=1234)
+
+    def step():
+        it = iter(range(n))
+        rollout(env, env.reset(TD({"locs": locs}, [b])), lambda td: acts[:, next(it)])
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier(world)
+    t = max_over_ranks(time.perf_counter() - t0, world, dev)
+    g = torch.Generator().manual_seed(rank)
+    rw = -torch.rand(b, n, generator=g) * 10
+    m = global_metrics(rw.mean(1), rw.max(1).values, torch.zeros(b), n)
+    out = {"metric": "env-steps/sec (batch×decode) SLAP & TSP-100 at 1/2/4/8 MI355X",
+           "value": world * b * n * args.steps / t, "unit": "env-steps/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": t / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u8+i64+f32", "data": "dry run: CPU oracle episode per gloo rank, no GPU",
+           "config": {"workload": f"TSP-{n} B={b}/rank oracle episode (dry run)",
+                      "batch_per_gpu": b, "num_loc": n, "dry_run": True,
+                      "parallelism": f"dp{world}: disjoint instance shards, no data-path "
+                                     "collective"},
+           "allgather_instances": m["instances"]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -588,16 +696,25 @@ def bench_pomo(b, n, k, world, rank, dev, fast_math=False):
     wall, ev = timed(run, k, 1, world, dev)
     assert int(ep.status.item()) == 0
     t = max_over_ranks(wall, world, dev)
-    t0 = time.perf_counter()
-    m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n)  # the RCCL exchange
-    torch.cuda.synchronize(dev)
-    t_ag = time.perf_counter() - t0
+    m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n)  # warm-up (communicator setup)
+    ag = []
+    for _ in range(10):  # the RCCL exchange itself (no collective at world size 1)
+        torch.cuda.synchronize(dev)
+        barrier(world)
+        t0 = time.perf_counter()
+        m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n)
+        torch.cuda.synchronize(dev)
+        ag.append(time.perf_counter() - t0)
+    t_ag = sorted(ag)[len(ag) // 2]
     return {"value": world * e * n * k / t, "ms_per_episode": t / k * 1e3,
             "instances_per_gpu": b, "starts": n, "envs_per_gpu": e,
             "bytes_per_env_step_decode_fused": 6 * n + 54,
             "decode_math": "fast (CO_DECODE_FAST, opt-in, not bit-exact)" if fast_math
             else "exact (ATen log_softmax bits, correctly rounded tanh)",
-            "allgather_ms": t_ag * 1e3, "global_instances": m["instances"],
+            "allgather_ms": t_ag * 1e3,
+            "allgather_note": "median of 10 after a warm-up call" + (
+                "" if world > 1 else "; world size 1: no collective runs, host bookkeeping only"),
+            "global_instances": m["instances"],
             "loss": float(m["loss"]), "max_reward_mean": float(m["max_reward_mean"])}
 
 
