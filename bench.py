@@ -537,6 +537,7 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
         return out
     ep = SLAPStepwiseEpisode(td, policy="closest").capture()
     wall, ev = timed(ep.replay, k, 2, world, dev)
+    assert int(ep.status.item()) == 0, "SLAP stepwise episode status"
     t = max_over_ranks(wall, world, dev)
     out["slap_stepwise_graph"] = {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "bytes_per_env_step": 234}
@@ -569,6 +570,7 @@ def bench_cvrp(b, n, k, world, rank, dev):
     run = lambda: next(cyc)(sh)  # noqa: E731
     kk = n_rot * max(1, (4 * k) // n_rot)
     wall, ev = timed(run, kk, n_rot, world, dev)
+    assert all(int(f.status.item()) == 0 for f in fus), "CVRP fused episode status"
     Ts = [f.final_state()["steps"] for f in fus]
     T = Ts[0]
     t = max_over_ranks(wall, world, dev)
@@ -584,7 +586,7 @@ def bench_cvrp(b, n, k, world, rank, dev):
     sw = CVRPStepwiseEpisode(td).capture()
     wall, ev = timed(sw.replay, k, 1, world, dev)
     t = max_over_ranks(wall, world, dev)
-    assert sw.T == T
+    assert sw.T == T and int(sw.status.item()) == 0, "CVRP stepwise episode status"
     steps_one = sum_over_ranks(b * T, world, dev)
     out["cvrp_stepwise_graph"] = {"value": steps_one * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "episode_steps": T,

@@ -41,8 +41,14 @@ class _GraphEpisode:
         return self
 
     def run_eager(self):
+        """One episode launched on the episode's stream, ordered after everything already
+        queued on the caller's stream (inputs written there) and before whatever the caller
+        queues next (reads of the outputs)."""
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):
             self._launch(self.stream.cuda_stream)
+        cur.wait_stream(self.stream)
 
     def replay(self):
         if self.graph is None:
