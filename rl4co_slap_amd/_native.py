@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import warnings
 import threading
 
 import torch
@@ -96,6 +97,10 @@ def load():
             fn.restype = ctypes.c_int
         lib.co_build_info.restype = ctypes.c_char_p
         lib.co_build_info.argtypes = []
+        if hasattr(lib, "co_variant_timing_cut"):
+            warnings.warn(f"rl4co_slap_amd: {LIB_PATH} is a timing-cut diagnostic build "
+                          "(CO_CVRP_CUT / CO_CVRP_RCUT): its results and status bits are not "
+                          "valid", RuntimeWarning, stacklevel=2)
         _lib = lib
         return lib
 

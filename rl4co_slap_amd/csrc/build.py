@@ -39,8 +39,10 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile each source to an object in parallel, then link the shared library."""
+def build(force=False, verbose: bool = False) -> str:
+    """Compile each source to an object in parallel, then link the shared library.
+    ``force="incremental"`` (``--incremental``) recompiles only objects older than their
+    source or a header (development); ``force=True`` recompiles everything."""
     from concurrent.futures import ThreadPoolExecutor
 
     if not force and not _stale():
@@ -51,8 +53,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
              "-fno-fast-math", "-Wall", "-Wno-unused-result", "-I", os.path.join(ROOT, "include")]
 
+    hdr_t = max(os.path.getmtime(d) for d in
+                [os.path.join(HERE, h) for h in HEADERS] + [os.path.join(ROOT, "include", "co_env.h")])
+    incremental = force == "incremental"
+
     def compile_one(src):
         obj = os.path.join(obj_dir, os.path.splitext(src)[0] + ".o")
+        if incremental and os.path.exists(obj):
+            t = os.path.getmtime(obj)
+            if t > hdr_t and t > os.path.getmtime(os.path.join(HERE, src)):
+                return obj  # object newer than its source and every header
         cmd = [hipcc()] + flags + ["-c", os.path.join(HERE, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
@@ -72,4 +82,5 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="incremental" if "--incremental" in sys.argv else "--force" in sys.argv,
+                verbose=True))

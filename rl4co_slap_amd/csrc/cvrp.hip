@@ -12,6 +12,13 @@
 
 using namespace co;
 
+#if CO_CVRP_CUT || CO_CVRP_RCUT
+// timing-diagnostic builds (tools/build_variants.sh) cut work out of the step / reward
+// kernels: their results and status bits are wrong by design.  The marker makes
+// _native.load() warn loudly for any library built this way.
+extern "C" __attribute__((visibility("default"))) const int co_variant_timing_cut = 1;
+#endif
+
 namespace {
 
 // Writes visited_out (optional update at column `a`), the action mask and returns
@@ -531,6 +538,254 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Reward + validity over step-major actions ([T, B] rows, what the stepwise episode
+// records; any strides work): 64 consecutive instances per workgroup, lane = instance,
+// so each action load of a wave is one coalesced 512-B piece of a row that no other
+// workgroup touches.  The tile's [64, N+1] coordinates (and, with `check`, its [64, N]
+// demand rows) are staged once into LDS by LDS-DMA.
+// * Walker waves split the steps into contiguous ranges (a range's first edge starts
+//   from the action before it), double-buffer U-step batches of action rows and sum the
+//   edges (f32 per batch, f64 across batches); they also flag out-of-range indices.
+// * With `check`, wave 0 is the scanner: it walks the whole episode in step order with
+//   a two-stage pipeline (batch k+1's action rows in flight -- L2 hits after the walkers
+//   -- while batch k is processed): marks the node in the instance's LDS visited words
+//   (no-return ds_or; the permutation test is "N nonzero steps and N distinct bits"),
+//   takes d_t from the LDS demand row (cvrp/env.py:177-178: -capacity at the depot) and
+//   runs the reference's sequential f32 capacity scan (cvrp/env.py:180-190) in its exact
+//   operation order.  Its serial chain overlaps the walkers instead of following them.
+#ifndef CO_CVRPR_U
+#define CO_CVRPR_U 8
+#endif
+#ifndef CO_CVRPR_Q
+#define CO_CVRPR_Q 8
+#endif
+#ifndef CO_CVRPR_SU
+#define CO_CVRPR_SU 8
+#endif
+struct CvrpRewardTile {  // LDS carve-up of cvrp_reward_tile_kernel (host + device)
+  int NC, VW;
+  size_t xy, dem, len, vis, ncap, total;
+  __host__ __device__ CvrpRewardTile(int N, int Q, int check) {
+    NC = N + 1;
+    VW = ((N + 32) >> 5) | 1;  // visited words per instance (odd stride)
+    const size_t dbytes = check ? (((size_t)64 * N * 4) + 15) & ~(size_t)15 : 0;
+    const size_t lbytes = (size_t)Q * 64 * 8;
+    size_t o = 0;
+    xy = o;   o += (((size_t)64 * NC * 8) + 15) & ~(size_t)15;
+    dem = len = o;  // the partial sums reuse the demand rows after the episode
+    o += dbytes > lbytes ? dbytes : lbytes;
+    vis = o;  o += check ? (size_t)64 * VW * 4 : 0;
+    ncap = o; o += check ? 64 * 4 : 0;  // -vehicle_capacity per instance (depot's term)
+    total = o;
+  }
+};
+
+template <int Q>
+__global__ __launch_bounds__(64 * Q) void cvrp_reward_tile_kernel(
+    int64_t B, int N, int T, const float2* __restrict__ locs, const int64_t* __restrict__ acts,
+    int64_t sb, int64_t st, const float* __restrict__ demand, const float* __restrict__ vcap,
+    int check, float* __restrict__ reward, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const CvrpRewardTile L(N, Q, check);
+  const int NC = N + 1;
+  const float2* s_xy = reinterpret_cast<const float2*>(smem + L.xy);
+  uint32_t* s_vis = reinterpret_cast<uint32_t*>(smem + L.vis);
+  double* s_len = reinterpret_cast<double*>(smem + L.len);
+  __shared__ float2 s_last[64];  // the point after step T-1 (closing edge)
+  __shared__ int s_lok[64], s_range[64], s_cnt[64], s_over[64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t row0 = (int64_t)blockIdx.x * 64;
+  const int rows = (int)((B - row0) < 64 ? (B - row0) : 64);
+  const bool live = lane < rows;
+  const int64_t b = live ? row0 + lane : row0;  // dead lanes mirror lane 0's loads
+  const int64_t* ap = acts + b * sb;             // this lane's column (row t at ap[t * st])
+#ifdef CO_CVRPR_TIMING  // diagnostic: phase clocks of each workgroup into reward[row0 + i]
+  __shared__ unsigned long long s_tm[8];
+  const unsigned long long tm0 = __builtin_readcyclecounter();
+  if (threadIdx.x < 8) s_tm[threadIdx.x] = 0;
+#endif
+  // roles; each issues its first action rows before the tiles are staged (the staging
+  // helper's vmcnt(0) + barrier then covers them too)
+  const bool scanner = check && q == 0;
+  constexpr int SU = CO_CVRPR_SU, U = CO_CVRPR_U;
+  const uint32_t* ap32 = reinterpret_cast<const uint32_t*>(ap);  // low dwords
+  const int64_t st2 = st * 2;
+  uint32_t a0[SU], a1[SU], a2[SU];
+  auto sload = [&](uint32_t (&dst)[SU], int t0) {  // scanner rows, clamped into [0, T)
+#pragma unroll
+    for (int u = 0; u < SU; ++u) dst[u] = ap32[(int64_t)(t0 + u < T ? t0 + u : T - 1) * st2];
+  };
+  const int P = check ? Q - 1 : Q;  // walker waves
+  const int p = check ? q - 1 : q;
+  const int R = (T + P - 1) / P;
+  const int m_lo = p * R < T ? p * R : T;
+  const int m_hi = m_lo + R < T ? m_lo + R : T;
+  int64_t bufA[U], bufB[U], a_prev = 0;
+  auto wload = [&](int64_t (&dst)[U], int t0) {  // walker rows, clamped into [m_lo, m_hi)
+#pragma unroll
+    for (int u = 0; u < U; ++u) dst[u] = ap[(int64_t)(t0 + u < m_hi ? t0 + u : m_hi - 1) * st];
+  };
+  if (scanner) {
+    sload(a0, 0);
+    sload(a1, SU);
+  } else if (m_lo < m_hi) {
+    if (m_lo > 0) a_prev = ap[(int64_t)(m_lo - 1) * st];
+    wload(bufA, m_lo);
+  }
+  if (check)
+    for (int k = threadIdx.x; k < 64 * L.VW; k += 64 * Q) s_vis[k] = 0u;
+  if (threadIdx.x < 64) s_range[threadIdx.x] = s_cnt[threadIdx.x] = 0;
+  if (check) {  // demand rows by LDS-DMA (walker waves), in flight with the coordinates
+    const unsigned char* dsrc = reinterpret_cast<const unsigned char*>(demand + row0 * N);
+    const int dbytes = rows * N * 4, d16 = dbytes & ~15;
+    for (int base = (q - 1) * 1024; q > 0 && base < d16; base += (Q - 1) * 1024)
+      if (base + lane * 16 < d16)
+        __builtin_amdgcn_global_load_lds((const void*)(dsrc + base + lane * 16),
+                                         (lds_void*)(smem + L.dem + base), 16, 0, 0);
+    for (int k = d16 + (int)threadIdx.x; k < dbytes; k += 64 * Q) smem[L.dem + k] = dsrc[k];
+  }
+  stage_bytes_lds(reinterpret_cast<const unsigned char*>(locs + row0 * NC), rows * NC * 8,
+                  smem + L.xy);  // ends with vmcnt(0) + a barrier
+  const float2* xy = s_xy + (size_t)lane * NC;
+#ifdef CO_CVRPR_TIMING
+  if (threadIdx.x == 0) s_tm[1] = __builtin_readcyclecounter() - tm0;
+#endif
+  double len = 0.0;
+  if (scanner) {
+    // ---- scanner (cvrp/env.py:177-190 in step order).  Only the low dword of each
+    // action is read: an index outside [0, N] makes the tour invalid (the walkers flag
+    // it), which overrides the capacity result, so it is only clamped here.  Node a's
+    // demand term is one LDS read without a branch: a == 0 reads the lane's
+    // -capacity slot instead of the demand row (cvrp/env.py:177).
+    const unsigned dem_base = (unsigned)(L.dem + (size_t)lane * N * 4) - 4u;  // node a at +4a
+    const unsigned cap_off = (unsigned)(L.ncap + lane * 4);
+    const float cap = vcap[b];
+    *reinterpret_cast<float*>(smem + cap_off) = -cap;
+    const float lim = cap + 1e-5f;
+    float used = 0.f;
+    bool over = false;
+    // cvrp/env.py:183-190 per step: used += d; used[used < 0] = 0; assert used <= cap +
+    // 1e-5.  As max(used + d, 0) the chain is two dependent VALU ops; max differs from
+    // the reference only for a NaN sum (the reference keeps NaN, which fails the assert),
+    // so a NaN sum is flagged as an overflow directly -- an overflow is final.  Steps
+    // past T (the last batch's padding) add +0.
+    auto scan = [&](const uint32_t (&src)[SU], int t0) {
+      float dv[SU];
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const uint32_t a = src[u] < (uint32_t)N ? src[u] : (uint32_t)N;
+        dv[u] = *reinterpret_cast<const float*>(smem + (a == 0 ? cap_off : dem_base + a * 4u));
+      }
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const float t = used + (t0 + u < T ? dv[u] : 0.f);
+        used = fmaxf(t, 0.f);
+        over |= !(used <= lim) | (t != t);
+      }
+    };
+    // three-deep batch pipeline: batches k+1 and k+2 in flight while k is scanned
+    const int nb = (T + SU - 1) / SU;
+    int k = 0;
+    for (; k + 2 < nb; k += 3) {
+      sload(a2, (k + 2) * SU);
+      scan(a0, k * SU);
+      sload(a0, (k + 3) * SU);
+      scan(a1, (k + 1) * SU);
+      sload(a1, (k + 4) * SU);
+      scan(a2, (k + 2) * SU);
+    }
+    if (k < nb) scan(a0, k * SU);
+    if (k + 1 < nb) scan(a1, (k + 1) * SU);
+    s_over[lane] = over;
+#ifdef CO_CVRPR_TIMING
+    if (lane == 0) s_tm[2] = __builtin_readcyclecounter() - tm0;
+#endif
+  } else {
+    // ---- walkers: edges (+ visited words) over a contiguous step range
+    bool range = false;
+    int nonzero = 0;
+    uint32_t* vw = s_vis + lane * L.VW;
+    if (m_lo < m_hi) {
+      // the point before the range: the depot at m = 0, else the previous step's node
+      bool pok = a_prev >= 0 && a_prev <= N;
+      float2 pt = xy[pok ? (int)a_prev : 0];
+      auto run = [&](const int64_t (&src)[U], int t0) {
+        const int cnt = m_hi - t0 < U ? m_hi - t0 : U;  // wave-uniform
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < cnt) {
+            const bool ok = src[u] >= 0 && src[u] <= N;
+            const int a = ok ? (int)src[u] : 0;
+            const float2 qq = xy[a];
+            if (check) {  // no-return ds_or; node 0 (depot / out of range) is not counted
+              __hip_atomic_fetch_or(&vw[a >> 5], 1u << (a & 31), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+              nonzero += a != 0;
+            }
+            if (pok && ok) {
+              const float dx = qq.x - pt.x, dy = qq.y - pt.y;
+              acc += sqrtf(dx * dx + dy * dy);
+            }
+            range |= !ok;
+            pt = qq;
+            pok = ok;
+          }
+        }
+        len += (double)acc;
+      };
+      const int nb = (m_hi - m_lo + U - 1) / U;
+      int k = 0;
+      for (; k + 1 < nb; k += 2) {
+        wload(bufB, m_lo + (k + 1) * U);
+        run(bufA, m_lo + k * U);
+        if (k + 2 < nb) wload(bufA, m_lo + (k + 2) * U);
+        run(bufB, m_lo + (k + 1) * U);
+      }
+      if (k < nb) run(bufA, m_lo + k * U);
+      if (m_hi == T) {  // owner of the last step: the closing edge starts here
+        s_last[lane] = pt;
+        s_lok[lane] = pok;
+      }
+    }
+    if (range) s_range[lane] = 1;
+    if (check && nonzero) atomicAdd(&s_cnt[lane], nonzero);
+#ifdef CO_CVRPR_TIMING
+    if (lane == 0) atomicMax(&s_tm[3], __builtin_readcyclecounter() - tm0);
+#endif
+  }
+  const float2 dep = xy[0];
+  __syncthreads();  // episode walked: the demand rows are free for the partial sums
+  s_len[q * 64 + lane] = len;  // the scanner's entry is 0
+  __syncthreads();
+  if (q == 0) {
+    const bool rng = live && s_range[lane];
+    if (live) {
+      double tot = 0.0;
+#pragma unroll
+      for (int w = 0; w < Q; ++w) tot += s_len[w * 64 + lane];
+      if (s_lok[lane]) tot += (double)edge_len(s_last[lane].x, s_last[lane].y, dep.x, dep.y);
+      reward[b] = -(float)tot;
+    }
+    // status bits are batch-wide: one atomic per bit per workgroup
+    if (__any(rng) && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
+    if (check) {  // a permutation of 1..N among the steps: N nonzero steps, N distinct bits
+      const uint32_t* vw = s_vis + lane * L.VW;
+      int bits = -(int)(vw[0] & 1u);  // node 0 (the depot) is not a customer
+      for (int w = 0; w < L.VW; ++w) bits += __popc(vw[w]);
+      const bool invalid = live && (rng || s_cnt[lane] != N || bits != N);
+      const bool ovr = live && !invalid && s_over[lane];
+      if (__any(invalid) && lane == 0) set_status(status, CO_ST_INVALID_TOUR);
+      if (__any(ovr) && lane == 0) set_status(status, CO_ST_OVER_CAPACITY);
+    }
+#ifdef CO_CVRPR_TIMING
+    if (lane == 0) s_tm[4] = __builtin_readcyclecounter() - tm0;
+    if (lane < 5 && lane < rows) reward[row0 + lane] = (float)s_tm[lane];
+#endif
+  }
+}
+
 }  // namespace
 
 extern "C" int co_cvrp_reset(int64_t B, int64_t N, const float* depot, const float* locs_in,
@@ -604,27 +859,30 @@ extern "C" int co_cvrp_reward(int64_t B, int64_t N, int64_t T, const float* locs
   if (!locs || !actions || !reward) return CO_E_INVAL;
   if (check && (!demand || !vcap || !status)) return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  // step-major actions (or a row-major episode too long for the wave-per-instance
+  // kernel's LDS sequence) and a 16-B aligned coordinate tensor: the tile kernel
+  constexpr int kQ = CO_CVRPR_Q;
   const size_t per_wave = check ? (size_t)((N + 32) / 32 + 4 * T) * 4 : 0;
-  // step-major actions ([T, B] rows): 16 consecutive instances per workgroup, so each
-  // 128-B line of an action row is consumed on one CU (4 per workgroup spread a line over
-  // 4 XCDs' L2s: 160 MB read per launch at B = 32,768, T = 112, vs ~70 MB algorithmic)
-  int waves = (sb == 1 && st == B) ? 16 : 4;
+  const bool step_major = sb == 1 && st == B;
+  const size_t tile_lds = CvrpRewardTile((int)N, kQ, check).total;
+  if ((step_major || per_wave > 64 * 1024) &&
+      ((reinterpret_cast<uintptr_t>(locs) | (check ? reinterpret_cast<uintptr_t>(demand) : 0)) &
+       15) == 0 &&
+      tile_lds <= 80 * 1024) {
+    hipLaunchKernelGGL(cvrp_reward_tile_kernel<kQ>, dim3((unsigned)((B + 63) / 64)),
+                       dim3(64 * kQ), tile_lds, (hipStream_t)stream, B, (int)N, (int)T,
+                       reinterpret_cast<const float2*>(locs), actions, sb, st, demand, vcap,
+                       check, reward, status);
+    return launch_status();
+  }
+  // row-major actions: one wave per instance, lanes over steps (coalesced rows)
+  int waves = 4;
   while (waves > 1 && per_wave * waves > 64 * 1024) waves >>= 1;
   if (per_wave > 64 * 1024) return CO_E_INVAL;
   const size_t shmem = per_wave * waves;
   const dim3 grid(grid_for(B, waves, 256 * 32));
   const float2* l2 = reinterpret_cast<const float2*>(locs);
   switch (waves) {
-    case 16:
-      hipLaunchKernelGGL(cvrp_reward_kernel<16>, grid, dim3(1024), shmem, (hipStream_t)stream,
-                         B, (int)N, (int)T, l2, actions, sb, st, demand, vcap, check, reward,
-                         status);
-      break;
-    case 8:
-      hipLaunchKernelGGL(cvrp_reward_kernel<8>, grid, dim3(512), shmem, (hipStream_t)stream, B,
-                         (int)N, (int)T, l2, actions, sb, st, demand, vcap, check, reward,
-                         status);
-      break;
     case 4:
       hipLaunchKernelGGL(cvrp_reward_kernel<4>, grid, dim3(256), shmem, (hipStream_t)stream, B,
                          (int)N, (int)T, l2, actions, sb, st, demand, vcap, check, reward,

@@ -331,15 +331,31 @@ def _oracle_over(demand, actions):
 
 @pytest.mark.parametrize("step_major", [False, True])
 def test_cvrp_reward_capacity_scan_routes(dev, step_major):
-    """The route-parallel capacity scan equals the reference's sequential scan per row,
-    including routes that end in (cap, cap + 1e-5] and leave a residual for the next one
-    (the lane-0 sequential repeat) -- rows checked one launch each (status is batch-wide)."""
+    """Both reward kernels' capacity scans equal the reference's sequential scan per row
+    (row-major actions: the route-split scan, lanes over routes, repeated passes until no
+    route start changes; step-major: the tile kernel's sequential scan), including routes
+    that end in (cap, cap + 1e-5] and leave a residual for the next one, a chain of three
+    such routes (three passes), and a row of more than 64 routes (lanes owning two routes
+    each) -- rows checked one launch each (status is batch-wide)."""
     g = torch.Generator().manual_seed(17)
     rows = []
     # residual 3.8e-6 after route 1; route 2 overflows only with it / fits even with it
     for tail, want in (([0.5, 0.500008], True), ([0.5, 0.5], False)):
         dm = torch.tensor([[0.5, 0.5000038] + tail])
         rows.append((dm, torch.tensor([[1, 2, 0, 3, 4, 0, 0]]), want))
+    # a chain of residual routes: 3.8e-6 left after each of routes 1 and 2, so route 3 of
+    # the same demands overflows only through the chain (1 + 3 x 3.8e-6 > 1 + 1e-5) while
+    # a route 3 of [0.5, 0.5] still fits
+    for tail, want in (([0.5, 0.5000038], True), ([0.5, 0.5], False)):
+        dm = torch.tensor([[0.5, 0.5000038, 0.5, 0.5000038] + tail])
+        rows.append((dm, torch.tensor([[1, 2, 0, 3, 4, 0, 5, 6, 0, 0]]), want))
+    # 140 single-customer routes (> 64 routes per row), one of them over capacity or not
+    for over_at in (None, 137):
+        dm = torch.full((1, 140), 0.25)
+        if over_at is not None:
+            dm[0, over_at] = 1.5
+        acts = torch.stack([torch.arange(1, 141), torch.zeros(140, dtype=torch.int64)], 1)
+        rows.append((dm, acts.reshape(1, -1), over_at is not None))
     for r in range(40):
         n = int(torch.randint(5, 40, (1,), generator=g))
         dm = (torch.randint(1, 10, (1, n), generator=g).float() / 10.0)
@@ -365,3 +381,71 @@ def test_cvrp_reward_capacity_scan_routes(dev, step_major):
         assert not st & 1
         n_over += over
     assert 3 <= n_over < len(rows)
+
+
+def _cvrp_oracle_reward(locs, demand, actions):
+    td = TD({"locs": locs, "demand": demand,
+             "vehicle_capacity": torch.ones(demand.shape[0], 1)}, [demand.shape[0]])
+    return CVRPOracle._get_reward(None, td, actions)
+
+
+def _cvrp_random_tours(b, n, extra, seed):
+    """Valid tours over n customers with `extra` additional depot visits spread through
+    them (row-major [b, n + extra]) and demands that make some rows overflow."""
+    g = torch.Generator().manual_seed(seed)
+    T = n + extra
+    acts = torch.zeros(b, T, dtype=torch.int64)
+    for r in range(b):
+        slots = torch.randperm(T, generator=g)[:n].sort()[0]
+        acts[r, slots] = torch.randperm(n, generator=g) + 1
+    dm = torch.randint(1, 10, (b, n), generator=g).float() / 30.0
+    locs = torch.rand(b, n + 1, 2, generator=g)
+    return locs, dm, acts
+
+
+@pytest.mark.parametrize("b,n,extra", [(1, 5, 3), (70, 10, 1490), (300, 100, 12), (64, 100, 60)])
+@pytest.mark.parametrize("step_major", [False, True])
+def test_cvrp_reward_tile_kernel_vs_oracle(dev, b, n, extra, step_major):
+    """Rewards of both layouts vs the oracle's tour length; the validity/capacity status
+    of the whole batch vs the oracle's asserts.  T = 1,500 makes the step-major tile
+    kernel split the episode into chunks (its LDS demand sequence holds ~290 steps at
+    N = 10), carrying the capacity scan across them; B = 70 / 300 leave partial tiles."""
+    locs, dm, acts = _cvrp_random_tours(b, n, extra, 1000 + b + n)
+    r, st = _cvrp_reward_status(dev, locs, acts, dm, step_major)
+    assert_reward_close(r, _cvrp_oracle_reward(locs, dm, acts))
+    assert bool(st & 2) == _oracle_over(dm, acts)
+    assert not st & 1
+    # per row: the status is batch-wide, so compare row by row on a few rows
+    for row in range(min(b, 6)):
+        _, st1 = _cvrp_reward_status(dev, locs[row:row + 1], acts[row:row + 1],
+                                     dm[row:row + 1], step_major)
+        assert bool(st1 & 2) == _oracle_over(dm[row:row + 1], acts[row:row + 1]), row
+
+
+@pytest.mark.parametrize("step_major", [False, True])
+def test_cvrp_reward_long_episode_row_major_fallback(dev, step_major):
+    """T = 5,000 steps: beyond the wave-per-instance kernel's LDS sequence (64 KB), so
+    row-major actions also take the chunked tile kernel (no CO_E_INVAL)."""
+    locs, dm, acts = _cvrp_random_tours(3, 12, 4988, 77)
+    r, st = _cvrp_reward_status(dev, locs, acts, dm, step_major)
+    assert_reward_close(r, _cvrp_oracle_reward(locs, dm, acts))
+    assert bool(st & 2) == _oracle_over(dm, acts)
+    assert not st & 1
+
+
+@pytest.mark.parametrize("step_major", [False, True])
+def test_cvrp_reward_invalid_and_range(dev, step_major):
+    """Revisit, missing customer and out-of-range index through both kernels: the
+    reference's "Invalid tour" (and the gather's range error) as status bits."""
+    locs, dm, acts = _cvrp_random_tours(130, 20, 10, 5)
+    _, st = _cvrp_reward_status(dev, locs, acts, dm, step_major)
+    assert not st & 1
+    bad = acts.clone()
+    nz = (bad[77] != 0).nonzero()[:2, 0]
+    bad[77, nz[1]] = bad[77, nz[0]]  # revisit + a missing customer
+    _, st = _cvrp_reward_status(dev, locs, bad, dm, step_major)
+    assert st & 1
+    bad = acts.clone()
+    bad[129, 3] = 21  # out of range
+    _, st = _cvrp_reward_status(dev, locs, bad, dm, step_major)
+    assert st & 1 and st & 8

@@ -53,7 +53,8 @@ def test_cvrp100_config3_full_batch(dev):
     assert torch.equal(acts, ss["actions"].cpu())
     for k in ("visited", "action_mask", "used_capacity", "current_node", "done"):
         assert torch.equal(sf[k].cpu(), ss[k].cpu()), k
-    assert torch.equal(sf["reward"].cpu(), ss["reward"].cpu())
+    # the two engines' reward kernels sum the edges in different orders (tolerance 1e-5)
+    _close(sf["reward"].cpu(), ss["reward"].cpu())
     # every customer exactly once, depot padding after the last customer
     cust = torch.zeros(b, n + 1, dtype=torch.int64).scatter_add_(1, acts, torch.ones_like(acts))
     assert (cust[:, 1:] == 1).all()

@@ -45,3 +45,14 @@ for check in (1, 0):
     torch.cuda.synchronize(dev)
     out[f"check{check}_us"] = e0.elapsed_time(e1) * 1e3 / 30
 print(json.dumps(out))
+if os.environ.get("CO_TIMING"):  # a -DCO_CVRPR_TIMING build: per-workgroup phase clocks
+    f = nat.bind("co_cvrp_reward", b, n, T, nat.ptr(ep.locs), nat.ptr(acts), 1, b,
+                 nat.ptr(ep.demand), nat.ptr(ep.vcap_t), 1, nat.ptr(ep.reward),
+                 nat.ptr(ep.status))
+    f(s)
+    f(s)
+    torch.cuda.synchronize(dev)
+    tm = ep.reward.view(-1, 64)[:, :5].cpu().double()
+    names = ["start", "staged", "scanner_done", "walkers_done", "end"]
+    print(json.dumps({nm: [round(float(tm[:, i].quantile(p)), 0) for p in (0.1, 0.5, 0.9, 1.0)]
+                      for i, nm in enumerate(names)}))
