@@ -183,6 +183,92 @@ def copy_probe(traffic_bytes, dev, k):
     return res
 
 
+def time_bound(f, dev, reps=50):
+    """Average HIP-event time (s) of `reps` back-to-back launches of a bound C-ABI call."""
+    s = torch.cuda.current_stream(dev).cuda_stream
+    for _ in range(3):
+        f(s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        f(s)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
+def step_kernels_vs_copy(dev):
+    """Each stepwise env kernel alone (one launch = one env step over the batch, state
+    re-read from where the previous launch left it, as in the stepwise graphs) beside
+    co_probe_copy moving the same bytes through the same kind of buffer (one buffer pair
+    reused, i.e. Infinity-Cache resident like the stepwise state): the small-launch
+    ceiling a step kernel of that size can reach.  Bytes per env
+    step: SURVEY.md 8d (TSP 2N+50, CVRP 7N+33, SLAP 2L+34)."""
+    from rl4co_slap_amd import _native as nat
+
+    out = {}
+    d = dev
+
+    def copy_us(nbytes):
+        n = (nbytes // 2) // 16 * 16
+        a, c = torch.ones(n, dtype=torch.uint8, device=d), torch.empty(n, dtype=torch.uint8, device=d)
+        return time_bound(nat.bind("co_probe_copy", nat.ptr(a), nat.ptr(c), n), d) * 1e6
+
+    def rec(name, us, nbytes):
+        cu = copy_us(nbytes)
+        out[name] = {"bytes": nbytes, "kernel_us": us, "kernel_GBps": nbytes / us / 1e3,
+                     "copy_same_bytes_us": cu, "copy_GBps": nbytes / cu / 1e3,
+                     "frac_of_copy": cu / us, "hbm_frac": nbytes / us / 1e3 / HBM_PEAK_GBS}
+
+    # TSP-100, B = 65,536 (co_tsp_step, first_mode 0)
+    b, n = 65536, 100
+    act = torch.randint(0, n, (b,), device=d)
+    mask = torch.ones(b, n, dtype=torch.bool, device=d)
+    i = torch.zeros(b, 1, dtype=torch.int64, device=d)
+    first, cur = torch.zeros(b, dtype=torch.int64, device=d), torch.empty(b, dtype=torch.int64, device=d)
+    done, rw = torch.empty(b, dtype=torch.bool, device=d), torch.empty(b, dtype=torch.bool, device=d)
+    st = torch.zeros(1, dtype=torch.int32, device=d)
+    f = nat.bind("co_tsp_step", b, n, nat.ptr(act), nat.ptr(mask), nat.ptr(mask), nat.ptr(i),
+                 nat.ptr(i), nat.ptr(first), nat.ptr(first), nat.ptr(cur), nat.ptr(done),
+                 nat.ptr(rw), 0, None, nat.ptr(st))
+    rec("tsp_step_b65536", time_bound(f, d) * 1e6, b * (2 * n + 50))
+    del act, mask, i, first, cur, done, rw
+    # CVRP-100, B = 32,768 (co_cvrp_step, fused mask)
+    b = 32768
+    act = torch.randint(0, n + 1, (b,), device=d)
+    dem = torch.rand(b, n, device=d) * 0.1
+    used, used2 = torch.zeros(b, 1, device=d), torch.zeros(b, 1, device=d)
+    vcap = torch.ones(b, 1, device=d)
+    vis = torch.zeros(b, n + 1, dtype=torch.uint8, device=d)
+    cur = torch.empty(b, dtype=torch.int64, device=d)
+    done, rw = torch.empty(b, dtype=torch.bool, device=d), torch.empty(b, dtype=torch.bool, device=d)
+    m = torch.empty(b, n + 1, dtype=torch.bool, device=d)
+    f = nat.bind("co_cvrp_step", b, n, nat.ptr(act), nat.ptr(dem), nat.ptr(used), nat.ptr(used2),
+                 nat.ptr(vcap), nat.ptr(vis), nat.ptr(vis), nat.ptr(cur), nat.ptr(done), nat.ptr(rw),
+                 nat.ptr(m), nat.ptr(st), None)
+    rec("cvrp_step_b32768", time_bound(f, d) * 1e6, b * (7 * n + 33))
+    del act, dem, used, used2, vcap, vis, cur, done, rw, m
+    # SLAP, B = 16,384, L = 100, P = 20 (co_slap_step, in-place assignment)
+    b, l, pp = 16384, 100, 20
+    act = torch.randint(1, l, (b,), device=d)
+    tc = torch.arange(pp, dtype=torch.float32, device=d).repeat(b, 1)
+    asg = torch.full((b, pp), -1, dtype=torch.int32, device=d)
+    mask = torch.ones(b, l, dtype=torch.bool, device=d)
+    i = torch.zeros(b, 1, dtype=torch.int64, device=d)
+    done, rw = torch.empty(b, 1, dtype=torch.bool, device=d), torch.empty(b, 1, dtype=torch.bool, device=d)
+    f = nat.bind("co_slap_step", b, l, pp, nat.ptr(act), nat.ptr(tc), pp, nat.ptr(asg), nat.ptr(asg),
+                 nat.ptr(mask), nat.ptr(mask), nat.ptr(i), nat.ptr(i), nat.ptr(done), nat.ptr(rw),
+                 nat.ptr(st))
+    rec("slap_step_b16384", time_bound(f, d) * 1e6, b * (2 * l + 34))
+    # the bench policy fused with it (co_slap_closest_step): + depot distances 4L read
+    dd = torch.rand(b, l, device=d)
+    f = nat.bind("co_slap_closest_step", b, l, pp, nat.ptr(dd), nat.ptr(tc), pp, nat.ptr(asg),
+                 nat.ptr(asg), nat.ptr(mask), nat.ptr(mask), nat.ptr(act), nat.ptr(i), nat.ptr(i), nat.ptr(done),
+                 nat.ptr(rw), nat.ptr(st))
+    rec("slap_closest_step_b16384", time_bound(f, d) * 1e6, b * (6 * l + 34))
+    return out
+
+
 def cpu_threads():
     # the box's CPU share (OMP_NUM_THREADS is set to it on the GPU pool), not the whole host
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
@@ -403,6 +489,7 @@ def main():
         modes["tsp_cvrp_generate"] = bench_generate_uniform(b, n, dev)
         annotate_modes(modes, n, world)
         out["modes"] = modes
+        out["step_kernels_vs_copy"] = step_kernels_vs_copy(dev)
 
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline_tsp(locs_cpu, acts_cpu)
@@ -473,6 +560,7 @@ def annotate_modes(modes, n, world):
         "slap_fused_random": lambda m: 2354 / 20,
         "slap_fused_random_b65536": lambda m: 2354 / 20,
         "slap_stepwise_graph": lambda m: 234 + 1684 / 20,
+        "slap_stepwise_graph_teacher": lambda m: 234 + 1684 / 20,
         "pomo_tsp100": lambda m: 6 * n + 54,
         "pomo_tsp100_fast_math": lambda m: 6 * n + 54,
         "cvrp_fused_nearest": lambda m: (8 + 12 * n + 8 * m["episode_steps"] + 10 * (n + 1) + 25)
@@ -535,12 +623,25 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
     del frs
     if not stepwise:
         return out
+    # closest-free policy fused with each step (co_slap_closest_step: one launch per step)
     ep = SLAPStepwiseEpisode(td, policy="closest").capture()
     wall, ev = timed(ep.replay, k, 2, world, dev)
     assert int(ep.status.item()) == 0, "SLAP stepwise episode status"
     t = max_over_ranks(wall, world, dev)
     out["slap_stepwise_graph"] = {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3,
-                                  "batch_per_gpu": b, "bytes_per_env_step": 234}
+                                  "batch_per_gpu": b, "bytes_per_env_step": 234,
+                                  "launches_per_step": 1, "policy": "closest-free (fused)"}
+    del ep
+    # the env step alone (co_slap_step), teacher-forced random-feasible actions
+    torch.manual_seed(4321 + rank)
+    acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
+    ep = SLAPStepwiseEpisode(td, actions=acts, policy="teacher").capture()
+    wall, ev = timed(ep.replay, k, 2, world, dev)
+    assert int(ep.status.item()) == 0, "SLAP stepwise teacher episode status"
+    t = max_over_ranks(wall, world, dev)
+    out["slap_stepwise_graph_teacher"] = {"value": world * b * 20 * k / t,
+                                          "ms_per_episode": t / k * 1e3, "batch_per_gpu": b,
+                                          "bytes_per_env_step": 234, "launches_per_step": 1}
     return out
 
 

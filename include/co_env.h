@@ -228,6 +228,17 @@ int co_cvrp_nearest_action(int64_t batch, int64_t num_loc, const float* locs,
                            int64_t* action_out, void* stream);
 int co_slap_closest_free_action(int64_t batch, int64_t num_slots, const float* depot_loc_dist,
                                 const uint8_t* action_mask, int64_t* action_out, void* stream);
+/* The closest-free bench policy fused with SLAPEnv._step (slap/env.py:38-93): the
+ * action co_slap_closest_free_action would pick is written to action_out and applied
+ * as co_slap_step does (assign_out = assign_in with [b, p] = action; in-place allowed),
+ * in one launch.  Results identical to the two calls (which it falls back to when
+ * num_slots % 4 != 0, num_slots > 256 or the buffers are misaligned). */
+int co_slap_closest_step(int64_t batch, int64_t num_slots, int64_t n_products,
+                         const float* depot_loc_dist, const float* to_choose, int64_t tc_stride,
+                         const int32_t* assign_in, int32_t* assign_out, const uint8_t* mask_in,
+                         uint8_t* mask_out,
+                         int64_t* action_out, const int64_t* i_in, int64_t* i_out, uint8_t* done,
+                         uint8_t* reward, int32_t* status, void* stream);
 
 /* -------------------------------------------- fused episode rollouts */
 

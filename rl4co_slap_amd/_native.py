@@ -46,6 +46,8 @@ _SIGS = {
     "co_tsp_nearest_action": [_i64, _i64, _p, _p, _p, _i32, _p, _p],
     "co_cvrp_nearest_action": [_i64, _i64, _p, _p, _p, _p, _p],
     "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],
+    "co_slap_closest_step": [_i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                             _p, _p],
     "co_count_not_done": [_p, _i64, _p, _p],
     "co_probe_copy": [_p, _p, _i64, _p],
     "co_uniform_fill": [_p, _i64, _f32, _f32, _f32, _i32, _u64, _u64, _p],

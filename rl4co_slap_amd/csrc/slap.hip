@@ -23,10 +23,31 @@ __global__ __launch_bounds__(256) void slap_reset_kernel(int64_t B, int64_t L, i
                                                          float* ratio) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t k = t0; k < B * L; k += stride) mask[k] = (k % L) != 0;
+  // 16-byte units where the buffers allow it (the launcher checks alignment)
+  const bool vm = (reinterpret_cast<uintptr_t>(mask) & 15) == 0;
+  const int64_t nm = B * L, nm16 = vm ? nm >> 4 : 0;
+  for (int64_t k = t0; k < nm16; k += stride) {  // mask[b, l] = l != 0 (depot masked)
+    union {
+      uint4 v;
+      uint8_t c[16];
+    } u;
+    int64_t col = (k << 4) % L;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      u.c[j] = col != 0;
+      if (++col == L) col = 0;
+    }
+    reinterpret_cast<uint4*>(mask)[k] = u.v;
+  }
+  for (int64_t k = (nm16 << 4) + t0; k < nm; k += stride) mask[k] = (k % L) != 0;
   for (int64_t k = t0; k < B * P; k += stride) to_choose[k] = (float)(k % P);
-  if (ratio)
-    for (int64_t k = t0; k < B * L; k += stride) ratio[k] = 0.f;
+  if (ratio) {
+    const bool vr = (reinterpret_cast<uintptr_t>(ratio) & 15) == 0;
+    const int64_t nr4 = vr ? nm >> 2 : 0;
+    for (int64_t k = t0; k < nr4; k += stride)
+      reinterpret_cast<float4*>(ratio)[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t k = (nr4 << 2) + t0; k < nm; k += stride) ratio[k] = 0.f;
+  }
   for (int64_t b = t0; b < B; b += stride) {
     it[b] = 0;
     reward[b] = 0.f;
@@ -84,31 +105,51 @@ template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void slap_reward_kernel(
     int64_t B, int L, int P, int O, int K, const int32_t* assignment, const int64_t* picklist,
     const float2* locs, float* reward, int32_t* status) {
+  // LDS per wave: the instance's locations [L] and assignment [P] (staged by lane loads
+  // issued together with the picklist loads: one memory latency per instance instead of
+  // the picklist -> assignment -> location chain), then the pick points [S] and the
+  // per-order lengths [O].
   extern __shared__ float s_rew[];
   const int w = threadIdx.x >> 6, lane = lane_id();
   const int S = O * K;
-  float2* pts = reinterpret_cast<float2*>(s_rew) + w * (S + O);
+  float2* lxy = reinterpret_cast<float2*>(s_rew) + (size_t)w * (L + S + O + (P + 1) / 2);
+  float2* pts = lxy + L;
   float* olen = reinterpret_cast<float*>(pts + S);
+  int32_t* asg = reinterpret_cast<int32_t*>(olen + O);
   for (int64_t b = (int64_t)blockIdx.x * WAVES + w; b < B; b += (int64_t)gridDim.x * WAVES) {
     const int64_t* prow = picklist + b * (int64_t)S;
     const int32_t* arow = assignment + b * (int64_t)P;
     const float2* lrow = locs + b * (int64_t)L;
+    constexpr int PU = 4;  // picks per lane kept in registers (S <= 256); more: a loop
+    int64_t pk[PU];
+#pragma unroll
+    for (int u = 0; u < PU; ++u) pk[u] = lane + 64 * u < S ? prow[lane + 64 * u] : 0;
+    for (int c = lane; c < L; c += 64) lxy[c] = lrow[c];
+    for (int c = lane; c < P; c += 64) asg[c] = arow[c];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     bool range = false;
-    for (int s = lane; s < S; s += 64) {
-      int64_t p = prow[s];
-      if (p < 0) p += P;
-      int64_t loc = 0;
-      if (p < 0 || p >= P) {
-        range = true;
-      } else {
-        loc = arow[p];
-        if (loc < 0) loc += L;
-        if (loc < 0 || loc >= L) {
-          range = true;
-          loc = 0;
+    for (int s0 = 0; s0 < S; s0 += 64 * PU) {
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int s = s0 + lane + 64 * u;
+        if (s < S) {
+          int64_t p = s0 == 0 ? pk[u] : prow[s];
+          if (p < 0) p += P;  // python indexing of assignment[b, picklist] (slap/env.py:139)
+          int64_t loc = 0;
+          if (p < 0 || p >= P) {
+            range = true;
+          } else {
+            loc = asg[p];
+            if (loc < 0) loc += L;  // the -1 of an unassigned product wraps (locs[b, -1])
+            if (loc < 0 || loc >= L) {
+              range = true;
+              loc = 0;
+            }
+          }
+          pts[s] = lxy[loc];
         }
       }
-      pts[s] = lrow[loc];
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -124,7 +165,7 @@ __global__ __launch_bounds__(WAVES * 64) void slap_reward_kernel(
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
+    if (lane == 0) {  // orders added one by one in f32 (slap/env.py:136-142)
       float total = 0.f;
       for (int o = 0; o < O; ++o) total += -olen[o];
       reward[b] = total;
@@ -155,6 +196,88 @@ __global__ __launch_bounds__(256) void slap_closest_kernel(int64_t B, int L, con
   }
 }
 
+// Closest-free bench policy fused with the env step (one launch per stepwise step; the
+// same results as co_slap_closest_free_action + co_slap_step with an in-place
+// assignment).  16 lanes per instance, 16 instances per 256-thread workgroup; lane sl
+// owns 4-location units u = sl + 16 k (k < KU): one float4 of depot distances and one
+// u32 of mask bytes each, so a group's loads are 256-B coalesced row pieces.  The
+// masked argmin (inf where not free, ties -> lowest index: torch.argmin) is a float
+// group min then an index group min (grp_argmin_split); the owner lane's unit is
+// written back with the chosen byte cleared, every other unit unchanged; lane 0
+// applies the step's row epilogue (slap/env.py:38-93).
+template <int KU>
+__global__ __launch_bounds__(256) void slap_closest_step_kernel(
+    int64_t B, int L, int P, const float* __restrict__ dist, const uint8_t* __restrict__ mask_in,
+    uint8_t* __restrict__ mask_out, int64_t* __restrict__ action_out,
+    const float* __restrict__ to_choose, int64_t tc_stride, const int32_t* assign_in,
+    int32_t* assign, const int64_t* __restrict__ i_in, int64_t* __restrict__ i_out, uint8_t* __restrict__ done,
+    uint8_t* __restrict__ reward, int32_t* status) {
+  constexpr int G = 16;
+  const int sl = threadIdx.x & (G - 1);
+  const int64_t b = (int64_t)blockIdx.x * (256 / G) + (threadIdx.x / G);
+  const bool live = b < B;
+  const int64_t bb = live ? b : B - 1;  // dead groups mirror the last row (wave-uniform DPP)
+  const int U = L >> 2;                  // units per row (L % 4 == 0)
+  const float4* drow = reinterpret_cast<const float4*>(dist + bb * (int64_t)L);
+  const uint32_t* mrow = reinterpret_cast<const uint32_t*>(mask_in + bb * (int64_t)L);
+  float4 dv[KU];
+  uint32_t mv[KU];
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {  // all loads first, unconditional within the row
+    const int u = sl + G * k;
+    const int uc = u < U ? u : U - 1;
+    dv[k] = drow[uc];
+    mv[k] = mrow[uc];
+  }
+  int64_t it = 0;
+  if (sl == 0) it = i_in[bb];
+  const float prod = to_choose[bb * tc_stride];  // every lane (one broadcast line)
+  float best = __builtin_inff();
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    const int u = sl + G * k;
+    if (u < U) {
+      const float d4[4] = {dv[k].x, dv[k].y, dv[k].z, dv[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = ((mv[k] >> (8 * j)) & 0xffu) ? d4[j] : __builtin_inff();
+        if (d < best) {  // ascending index within the lane: strict < keeps the lowest
+          best = d;
+          bi = 4 * u + j;
+        }
+      }
+      if (bi == 0x7fffffff) bi = 4 * u;  // a lane whose candidates are all masked
+    }
+  }
+  grp_argmin_split<G>(best, bi);
+  if (!live) return;
+  int64_t p = (int64_t)(int)prod;  // .to(torch.int), slap/env.py:52
+  if (p < 0) p += P;
+  const bool p_ok = p >= 0 && p < P;
+  if (assign_in != assign)  // out of place: the group writes the row with [p] = action
+    for (int c = sl; c < P; c += G) assign[b * P + c] = c == p ? bi : assign_in[b * P + c];
+  uint32_t* mo = reinterpret_cast<uint32_t*>(mask_out + b * (int64_t)L);
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    const int u = sl + G * k;
+    if (u < U) {
+      const uint32_t clr = (bi >> 2) == u ? ~(0xffu << (8 * (bi & 3))) : ~0u;
+      mo[u] = mv[k] & clr;
+    }
+  }
+  if (sl == 0) {  // slap/env.py:50-62 (the row epilogue of co_slap_step)
+    action_out[b] = bi;
+    if (!p_ok)
+      set_status(status, CO_ST_INDEX_RANGE);
+    else if (assign_in == assign)
+      assign[b * P + p] = bi;
+    done[b] = it == (int64_t)(P - 1);
+    i_out[b] = it + 1;
+    reward[b] = 0;
+  }
+}
+
 }  // namespace
 
 extern "C" int co_slap_reset(int64_t B, int64_t L, int64_t P, uint8_t* mask, float* to_choose,
@@ -162,7 +285,7 @@ extern "C" int co_slap_reset(int64_t B, int64_t L, int64_t P, uint8_t* mask, flo
   if (B < 0 || L <= 0 || P <= 0) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!mask || !to_choose || !it || !reward) return CO_E_INVAL;
-  hipLaunchKernelGGL(slap_reset_kernel, dim3(grid_for(B * L, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(slap_reset_kernel, dim3(grid_for(B * L / 16 + 1, 256)), dim3(256), 0,
                      (hipStream_t)stream, B, L, P, mask, to_choose, it, reward, ratio);
   return launch_status();
 }
@@ -193,13 +316,14 @@ extern "C" int co_slap_reward(int64_t B, int64_t L, int64_t P, int64_t O, int64_
   if (B == 0) return CO_OK;
   if (!assignment || !picklist || !locs || !reward) return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
-  const size_t per_wave = (size_t)(O * K) * sizeof(float2) + (size_t)O * sizeof(float) + 8;
+  // per wave, in float2 units: locations L, picks S, order lengths O (as floats, rounded
+  // up to float2 with the assignment ints)
+  const size_t per_wave = (size_t)(L + O * K + O + (P + 1) / 2) * sizeof(float2);
   int waves = 4;
   while (waves > 1 && per_wave * waves > 64 * 1024) waves >>= 1;
   if (per_wave > 64 * 1024) return CO_E_INVAL;
   const dim3 grid(grid_for(B, waves, 256 * 32));
-  // stride per wave in float2 units is (S + O); keep the LDS request consistent with it
-  const size_t shmem = (size_t)waves * (size_t)(O * K + O) * sizeof(float2);
+  const size_t shmem = (size_t)waves * per_wave;
   const float2* l2 = reinterpret_cast<const float2*>(locs);
   switch (waves) {
     case 4:
@@ -224,6 +348,43 @@ extern "C" int co_slap_closest_free_action(int64_t B, int64_t L, const float* di
   if (!dist || !mask || !out) return CO_E_INVAL;
   hipLaunchKernelGGL(slap_closest_kernel, dim3(grid_for(B, 4, 256 * 32)), dim3(256), 0,
                      (hipStream_t)stream, B, (int)L, dist, mask, out);
+  return launch_status();
+}
+
+extern "C" int co_slap_closest_step(int64_t B, int64_t L, int64_t P, const float* dist,
+                                    const float* to_choose, int64_t tc_stride,
+                                    const int32_t* assign_in, int32_t* assign,
+                                    const uint8_t* mask_in, uint8_t* mask_out, int64_t* action_out,
+                                    const int64_t* i_in, int64_t* i_out, uint8_t* done,
+                                    uint8_t* reward, int32_t* status, void* stream) {
+  if (B < 0 || L <= 0 || P <= 0 || L > (1 << 30)) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!dist || !to_choose || !assign_in || !assign || !mask_in || !mask_out || !action_out || !i_in || !i_out ||
+      !done || !reward)
+    return CO_E_INVAL;
+  const bool vec = L % 4 == 0 && L <= 4 * 16 * 4 &&
+                   ((reinterpret_cast<uintptr_t>(dist) & 15) |
+                    ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) &
+                     3)) == 0;
+  if (!vec) {  // the two launches it fuses
+    int rc = co_slap_closest_free_action(B, L, dist, mask_in, action_out, stream);
+    if (rc != CO_OK) return rc;
+    return co_slap_step(B, L, P, action_out, to_choose, tc_stride, assign_in, assign, mask_in,
+                        mask_out, i_in, i_out, done, reward, status, stream);
+  }
+  const dim3 grid((unsigned)((B + 15) / 16));
+  const int units = (int)(L / 4), ku = (units + 15) / 16;
+#define CO_SLAP_CS(K)                                                                        \
+  hipLaunchKernelGGL(slap_closest_step_kernel<K>, grid, dim3(256), 0, (hipStream_t)stream, B, \
+                     (int)L, (int)P, dist, mask_in, mask_out, action_out, to_choose, tc_stride, \
+                     assign_in, assign, i_in, i_out, done, reward, status)
+  switch (ku) {
+    case 1: CO_SLAP_CS(1); break;
+    case 2: CO_SLAP_CS(2); break;
+    case 3: CO_SLAP_CS(3); break;
+    default: CO_SLAP_CS(4);
+  }
+#undef CO_SLAP_CS
   return launch_status();
 }
 

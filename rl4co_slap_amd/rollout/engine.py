@@ -107,7 +107,9 @@ class TSPStepwiseEpisode(_GraphEpisode):
 
 
 class SLAPStepwiseEpisode(_GraphEpisode):
-    """Reset + P x co_slap_step (in-place assignment) + co_slap_reward."""
+    """Reset + P x co_slap_step (in-place assignment) + co_slap_reward; with the
+    closest-free bench policy each step is one co_slap_closest_step launch (policy +
+    step), teacher-forced actions go through co_slap_step alone."""
 
     def __init__(self, td, actions=None, policy: str = "teacher"):
         locs = td["locs"]
@@ -139,16 +141,22 @@ class SLAPStepwiseEpisode(_GraphEpisode):
         b, l, p = self.b, self.l, self.p
         nat.call("co_slap_reset", b, l, p, nat.ptr(self.mask[0]), nat.ptr(self.to_choose),
                  nat.ptr(self.i[0]), nat.ptr(self.reset_reward), nat.ptr(self.ratio), s)
-        # the generator's -1 assignment is the episode's starting state
-        self.assign.copy_(self.assign0, non_blocking=True)
         for t in range(p):
             src, dst = t & 1, (t + 1) & 1
             a = self.acts[t]
-            if self.policy == "closest":
-                nat.call("co_slap_closest_free_action", b, l, nat.ptr(self.depot_dist),
-                         nat.ptr(self.mask[src]), nat.ptr(a), s)
             tc = self.to_choose[:, t:]
-            nat.call("co_slap_step", b, l, p, nat.ptr(a), nat.ptr(tc), p, nat.ptr(self.assign),
+            # the generator's -1 assignment is the episode's starting state: the first step
+            # writes out of place from it (the reference clones, slap/env.py:50), later ones
+            # in place
+            a_in = self.assign0 if t == 0 else self.assign
+            if self.policy == "closest":  # the bench policy fused with the step: one launch
+                nat.call("co_slap_closest_step", b, l, p, nat.ptr(self.depot_dist), nat.ptr(tc), p,
+                         nat.ptr(a_in), nat.ptr(self.assign), nat.ptr(self.mask[src]),
+                         nat.ptr(self.mask[dst]),
+                         nat.ptr(a), nat.ptr(self.i[src]), nat.ptr(self.i[dst]),
+                         nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.status), s)
+                continue
+            nat.call("co_slap_step", b, l, p, nat.ptr(a), nat.ptr(tc), p, nat.ptr(a_in),
                      nat.ptr(self.assign), nat.ptr(self.mask[src]), nat.ptr(self.mask[dst]),
                      nat.ptr(self.i[src]), nat.ptr(self.i[dst]), nat.ptr(self.done),
                      nat.ptr(self.step_reward), nat.ptr(self.status), s)

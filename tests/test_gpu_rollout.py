@@ -153,17 +153,21 @@ def test_slap_rollout_matches_oracle(dev, cls_name, b, policy):
 
 
 @pytest.mark.parametrize("aisles,locs,prods,orders", [(6, 8, 12, 9), (12, 15, 40, 25),
-                                                      (10, 10, 20, 20), (4, 5, 19, 7)])
+                                                      (10, 10, 20, 20), (4, 5, 19, 7),
+                                                      (7, 7, 20, 9)])
 @pytest.mark.parametrize("dist", ["grid", "random_ties"])
-def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist):
-    """Fused closest-free episode for every lane-group width (L = 48 -> 8 lanes, 100 -> 16,
-    180 -> 32), P close to L - 1 (a lane's sorted list runs dry), and depot distances
-    with many exact ties at random positions."""
+@pytest.mark.parametrize("cls_name", ["SLAPFusedEpisode", "SLAPStepwiseEpisode"])
+def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist, cls_name):
+    """Closest-free episodes for every lane-group width of the fused kernel (L = 48 -> 8
+    lanes, 100 -> 16, 180 -> 32), P close to L - 1 (a lane's sorted list runs dry), and
+    depot distances with many exact ties at random positions; the stepwise engine's
+    co_slap_closest_step (policy + step in one launch: 1 / 2 / 3 units of 4 locations
+    per lane; L = 49 takes its two-launch fallback)."""
     import numpy as np
 
+    import rl4co_slap_amd.rollout.engine as eng
     from oracle.envs import SLAPOracle, slap_closest_free_action
     from oracle.td import TD
-    from rl4co_slap_amd.rollout.engine import SLAPFusedEpisode
     from rl4co_slap_amd.td import TensorDict
 
     b = 77
@@ -176,8 +180,8 @@ def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist):
                                               generator=g).float() * 0.5
     td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
     r, tdf, a = ref_rollout(env, td, slap_closest_free_action)
-    ep = SLAPFusedEpisode(TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev),
-                          None, policy="closest")
+    ep = getattr(eng, cls_name)(TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev),
+                                None, policy="closest")
     ep.run_eager()
     torch.cuda.synchronize()
     assert int(ep.status.item()) == 0
