@@ -470,6 +470,9 @@ def main():
         modes["tsp_fused_nearest"] = {"value": world * b * n * k / t_n,
                                       "ms_per_episode": t_n / k * 1e3}
         del ne
+        # the drop-in API path (ConstructivePolicy + TSPEnv, one decode + one env launch
+        # per step, Python TensorDict plumbing)
+        modes["dropin_tsp100"] = bench_dropin(b, n, k, world, rank, dev)
         # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
         modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
         # the north star's "SLAP at batch 65,536" (fused episode only)
@@ -554,6 +557,7 @@ def annotate_modes(modes, n, world):
     GB/s and the fraction of the 8 TB/s peak."""
     per_step = {
         "tsp_stepwise_graph": lambda m: 2 * n + 50 + (16 * n + 4) / n,
+        "dropin_tsp100": lambda m: 2 * n + 50 + 5 * n + 16 + (16 * n + 4) / n,
         "tsp_fused_nearest": lambda m: (17 * n + 30) / n,
         "slap_fused_closest": lambda m: 2754 / 20,
         "slap_fused_closest_b65536": lambda m: 2754 / 20,
@@ -642,6 +646,42 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
     out["slap_stepwise_graph_teacher"] = {"value": world * b * 20 * k / t,
                                           "ms_per_episode": t / k * 1e3, "batch_per_gpu": b,
                                           "bytes_per_env_step": 234, "launches_per_step": 1}
+    return out
+
+
+def bench_dropin(b, n, k, world, rank, dev):
+    """The path an unchanged rl4co policy takes:
+    ``ConstructivePolicy(None, LogitsDecoder(stub)).forward(td, TSPEnv, greedy)`` at
+    TSP-100 B=65,536 -- per step one co_decode_step launch (greedy, logits from a fixed
+    HBM-resident [B, N] tensor: the stub decoder) and one TSPEnv._step launch, the
+    TensorDict plumbing in Python, the done poll only from step N on (env lower bound),
+    then get_reward + validity and get_log_likelihood.  Also the host cost alone: the same
+    loop at B = 64, where the device work is negligible."""
+    from rl4co_slap_amd.envs import TSPEnv
+    from rl4co_slap_amd.rollout.constructive import ConstructivePolicy, LogitsDecoder
+    from rl4co_slap_amd.td import TensorDict
+
+    out = {}
+    for bb, kk in ((b, k), (64, 3 * k)):
+        locs, _ = tsp_inputs(bb, n, rank)
+        locs = locs.to(dev)
+        g = torch.Generator().manual_seed(7 + rank)
+        logits = torch.randn(bb, n, generator=g).to(dev)
+        env = TSPEnv(generator_params=dict(num_loc=n), device=dev)
+        pol = ConstructivePolicy(None, LogitsDecoder(lambda td: logits), env_name="tsp")
+
+        def run():
+            td = env.reset(TensorDict({"locs": locs}, [bb]))
+            return pol(td, env, phase="test", decode_type="greedy")
+
+        wall, _ = timed(run, kk, 2, world, dev)
+        t = max_over_ranks(wall, world, dev)
+        if bb == b:
+            out = {"value": world * bb * n * kk / t, "ms_per_episode": t / kk * 1e3,
+                   "batch_per_gpu": bb, "launches_per_step": 2,
+                   "done_polls_per_episode": 1, "path": "ConstructivePolicy.forward + TSPEnv"}
+        else:
+            out["host_us_per_step_b64"] = t / kk / n * 1e6
     return out
 
 

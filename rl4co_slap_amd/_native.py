@@ -99,7 +99,7 @@ def load():
             fn.restype = ctypes.c_int
         lib.co_build_info.restype = ctypes.c_char_p
         lib.co_build_info.argtypes = []
-        if hasattr(lib, "co_variant_timing_cut"):
+        if hasattr(lib, "co_variant_timing_cut") or hasattr(lib, "co_variant_timing_cut_decode"):
             warnings.warn(f"rl4co_slap_amd: {LIB_PATH} is a timing-cut diagnostic build "
                           "(CO_CVRP_CUT / CO_CVRP_RCUT): its results and status bits are not "
                           "valid", RuntimeWarning, stacklevel=2)

@@ -32,6 +32,10 @@ using namespace co;
 #ifndef CO_DECODE_UNR
 #define CO_DECODE_UNR 1
 #endif
+#if defined(CO_DIAG_FASTTANH) || defined(CO_DIAG_FASTEXP)
+// timing-diagnostic build: the "exact" decode is not exact (see _native.load())
+extern "C" __attribute__((visibility("default"))) const int co_variant_timing_cut_decode = 1;
+#endif
 __device__ __forceinline__ float co_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 // CO_DECODE_FAST (opt-in, mode flag): tanh(x) = 1 - 2 / (e^{2x} + 1) on v_exp / v_rcp (abs
 // error ~1e-7, exact +-1 saturation), the softmax exps on v_exp_f32 (<= 2 ulp) summed in
@@ -49,6 +53,9 @@ constexpr int kOptClip = 1, kOptTemp = 2, kOptFast = 4;
 
 template <int OPT>
 __device__ __forceinline__ float clip_tanh(float x) {
+#ifdef CO_DIAG_FASTTANH  // timing diagnostic: fast tanh inside the exact path
+  return co_tanh_fast(x);
+#endif
   return (OPT & kOptFast) ? co_tanh_fast(x) : tanh_cr(x);
 }
 
@@ -59,7 +66,11 @@ __device__ __forceinline__ float row_log_sum_exp(const float (&d)[EPL], int N, i
                                                  float* lds_row) {
   const int c0 = sl * EPL;
   float e[EPL];
+#ifdef CO_DIAG_FASTEXP  // timing diagnostic: fast exp-sum inside the exact path
+  if (true) {
+#else
   if (OPT & kOptFast) {
+#endif
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) s += c0 + k < N ? co_exp_fast(d[k]) : 0.f;

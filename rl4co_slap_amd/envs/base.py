@@ -70,6 +70,9 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         # host-side knowledge of td["i"] tensors this env produced:
         # id(tensor) -> (weakref, version, uniform value)
         self._i_known = {}
+        # lower bounds on the steps before `done` can be all true, keyed by the state
+        # tensor the bound is about (same weakref/version bookkeeping)
+        self._lb_known = {}
 
     # -- seeding (base.py:288-291) ---------------------------------------------
     def set_seed(self, seed: Optional[int]):
@@ -201,3 +204,28 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         if rec is None or rec[0]() is not t or rec[1] != t._version:
             return None
         return rec[2]
+
+    # -- done-poll lower bounds ---------------------------------------------------
+    def _remember_lb(self, t: torch.Tensor, steps: int):
+        if len(self._lb_known) > 64:
+            self._lb_known = {k: v for k, v in self._lb_known.items() if v[0]() is not None}
+        self._lb_known[id(t)] = (weakref.ref(t), t._version, max(int(steps), 0))
+
+    def _known_lb(self, t) -> Optional[int]:
+        if not isinstance(t, torch.Tensor):
+            return None
+        rec = self._lb_known.get(id(t))
+        if rec is None or rec[0]() is not t or rec[1] != t._version:
+            return None
+        return rec[2]
+
+    def min_steps_to_done(self, td) -> int:
+        """A host-side lower bound on the env steps still needed before every instance
+        of ``td`` can be done (0 = unknown: poll).  The decode loop skips the
+        ``td["done"].all()`` host sync while fewer steps than this have been taken,
+        which cannot change when it stops (``constructive/base.py:245``).  The bound
+        comes from state tensors this env produced itself and nobody modified since
+        (TSP: unvisited nodes, CVRP: unvisited nodes incl. the depot, SLAP: products
+        left); anything else gives 0."""
+        return 0
+

@@ -105,6 +105,7 @@ class CVRPEnv(RL4COEnvBase):
                  float(self.generator.vehicle_capacity), nat.ptr(locs_out), nat.ptr(cur),
                  nat.ptr(used), nat.ptr(vcap), nat.ptr(visited), nat.ptr(mask),
                  nat.stream_of(demand))
+        self._remember_lb(visited, n + 1)  # done = all N+1 nodes visited (cvrp/env.py:95)
         return TensorDict({"locs": locs_out, "demand": demand, "current_node": cur,
                            "used_capacity": used, "vehicle_capacity": vcap, "visited": visited,
                            "action_mask": mask}, batch_size=batch_size)
@@ -131,9 +132,17 @@ class CVRPEnv(RL4COEnvBase):
                  nat.ptr(used_out), nat.ptr(vcap), nat.ptr(visited), nat.ptr(visited_out),
                  nat.ptr(cur), nat.ptr(done), nat.ptr(reward), nat.ptr(mask), None, None,
                  nat.stream_of(demand))
+        lb = self._known_lb(td["visited"])
+        if lb is not None:  # a step marks at most one more node visited
+            self._remember_lb(visited_out, lb - 1)
         td.update({"current_node": cur, "used_capacity": used_out, "visited": visited_out,
                    "reward": reward, "done": done, "action_mask": mask})
         return td
+
+    def min_steps_to_done(self, td) -> int:
+        """done = every node incl. the depot visited; a step visits one node."""
+        return self._known_lb(td.get_raw("visited") if hasattr(td, "get_raw")
+                              else td["visited"]) or 0
 
     @staticmethod
     def get_action_mask(td: TensorDict) -> torch.Tensor:

@@ -130,6 +130,7 @@ class SLAPEnv(RL4COEnvBase):
         ratio = torch.empty(td["depot_loc_dist"].shape, dtype=torch.float32, device=dev)
         nat.call("co_slap_reset", b, l, p, nat.ptr(mask), nat.ptr(to_choose), nat.ptr(i),
                  nat.ptr(reward), nat.ptr(ratio), nat.stream_of(assignment))
+        self._remember_lb(i, p)  # done = (i == P-1) before the step (slap/env.py:57)
         return TensorDict({"assignment": assignment, "to_choose": to_choose, "i": i,
                            "ratio": ratio, "action_mask": mask, "reward": reward},
                           batch_size=batch_size)
@@ -155,6 +156,9 @@ class SLAPEnv(RL4COEnvBase):
                  nat.ptr(assign), nat.ptr(assign_out), nat.ptr(mask), nat.ptr(mask_out),
                  nat.ptr(i), nat.ptr(i_out), nat.ptr(done), nat.ptr(reward), None,
                  nat.stream_of(mask))
+        lb = self._known_lb(td["i"])
+        if lb is not None:
+            self._remember_lb(i_out, lb - 1)
         td.update({"assignment": assign_out, "to_choose": tc[..., 1:], "action_mask": mask_out,
                    "i": i_out, "reward": reward, "done": done})
         return td
@@ -179,3 +183,7 @@ class SLAPEnv(RL4COEnvBase):
 
     def get_action_mask(self, td):
         return td["action_mask"]
+
+    def min_steps_to_done(self, td) -> int:
+        """done = (i == P - 1) at the step (``slap/env.py:57``): P - i steps."""
+        return self._known_lb(td.get_raw("i") if hasattr(td, "get_raw") else td["i"]) or 0

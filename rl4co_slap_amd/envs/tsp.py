@@ -57,6 +57,7 @@ class TSPEnv(RL4COEnvBase):
         nat.call("co_tsp_reset", b, n, nat.ptr(mask), nat.ptr(cur), nat.ptr(cur), nat.ptr(i),
                  nat.ptr(reward), nat.stream_of(locs))
         self._remember_i(i, 0)
+        self._remember_lb(mask, n)  # N ones; a step clears at most one
         return TensorDict({"locs": locs, "first_node": cur, "current_node": cur, "i": i,
                            "action_mask": mask, "reward": reward}, batch_size=batch_size)
 
@@ -92,13 +93,19 @@ class TSPEnv(RL4COEnvBase):
                  nat.ptr(done), nat.ptr(reward), mode, nat.ptr(flag), None, nat.stream_of(mask))
         if known is not None:
             self._remember_i(i_out, known + 1)
+        lb = self._known_lb(td["action_mask"])
+        if lb is not None:
+            self._remember_lb(mask_out, lb - 1)
         td.update({"first_node": first_out, "current_node": td["action"], "i": i_out,
                    "action_mask": mask_out, "reward": reward, "done": done})
         return td
 
     def _get_reward(self, td, actions, check: bool = False) -> torch.Tensor:
-        """``tsp/env.py:157-173``: -tour length, fused with the permutation check."""
-        locs = td["locs"]
+        """``tsp/env.py:157-173``: -tour length, fused with the permutation check.  A
+        multistart td's un-replicated ``locs`` (``RepeatedRows``) is read in place: env
+        ``e`` uses coordinate row ``e % B`` (the kernel's ``locs_batch``)."""
+        raw = td.get_raw("locs") if hasattr(td, "get_raw") else td["locs"]
+        locs = getattr(raw, "base", raw)
         nat.require_device(locs, actions)
         locs = locs.contiguous()
         if actions.dtype != torch.int64:
@@ -121,6 +128,11 @@ class TSPEnv(RL4COEnvBase):
 
     def get_action_mask(self, td):
         return td["action_mask"]
+
+    def min_steps_to_done(self, td) -> int:
+        """done = no unvisited node (``tsp/env.py:78``), and a step clears one node."""
+        return self._known_lb(td.get_raw("action_mask") if hasattr(td, "get_raw")
+                              else td["action_mask"]) or 0
 
     def replace_selected_actions(self, cur_actions, new_actions, selection_mask):
         cur_actions[selection_mask] = new_actions[selection_mask]

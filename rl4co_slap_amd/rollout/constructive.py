@@ -7,8 +7,10 @@ num_starts) -> (logits, mask)`` with an optional ``decoder.pre_decoder_hook(td, 
 hidden, num_starts)``.  Everything between them is the hot path: the decoding step
 (``co_decode_step``: tanh clip, mask, temperature, log-softmax, greedy / sampling /
 evaluate selection in one launch), ``env.step`` on the env kernels, the multistart
-hooks and the episode reward.  As in the reference, ``while not td["done"].all()``
-reads the done flags once per step.
+hooks and the episode reward.  ``while not td["done"].all()`` (a host sync) is read
+only from the step on which the env's host-side lower bound
+(``env.min_steps_to_done``: e.g. N unvisited TSP nodes after reset) allows every
+instance to be done -- the same stopping step as the reference's per-step poll.
 """
 from __future__ import annotations
 
@@ -101,12 +103,16 @@ class ConstructivePolicy(nn.Module):
             mask_logits=decoding_kwargs.pop("mask_logits", self.mask_logits),
             store_all_logp=decoding_kwargs.pop("store_all_logp", return_entropy),
             **decoding_kwargs)
+        # steps that must happen before every instance can be done: the `done` poll (a host
+        # sync) is skipped until then, which cannot change where the loop stops
+        lb = env.min_steps_to_done(td) if hasattr(env, "min_steps_to_done") else 0
         td, env, num_starts = strategy.pre_decoder_hook(td, env)
+        lb -= len(strategy.actions)  # the multistart hook's first step
         hook = getattr(self.decoder, "pre_decoder_hook", None)
         if hook is not None:
             td, env, hidden = hook(td, env, hidden, num_starts)
         step = 0
-        while not td["done"].all():
+        while step < lb or not td["done"].all():
             logits, mask = self.decoder(td, hidden, num_starts)
             td = strategy.step(logits, mask, td,
                                action=actions[..., step] if actions is not None else None)

@@ -10,6 +10,33 @@ from __future__ import annotations
 
 import torch
 
+class RepeatedRows:
+    """A batchified ``[S*B, ...]`` entry kept as its ``[B, ...]`` rows (multistart layout
+    ``e = s*B + b`` reads row ``e % B``): ``batchify`` (``rl4co/utils/ops.py:16``,
+    ``x.expand(S, ...).contiguous()``) stores entries this way, and the copy is made only
+    when something reads the entry through the TensorDict.  The env kernels that accept
+    the row-index scheme (the TSP reward's ``locs_batch``) read ``base`` directly
+    (``TensorDict.get_raw``), so an unread ``locs`` is never replicated (655 MB at POMO
+    config 5 on one GPU)."""
+
+    __slots__ = ("base", "repeats")
+
+    def __init__(self, base: torch.Tensor, repeats: int):
+        self.base, self.repeats = base, repeats
+
+    @property
+    def shape(self):
+        return torch.Size((self.repeats * self.base.shape[0], *self.base.shape[1:]))
+
+    @property
+    def device(self):
+        return self.base.device
+
+    def materialize(self) -> torch.Tensor:
+        s = self.base.shape
+        return self.base.expand(self.repeats, *s).contiguous().view(s[0] * self.repeats, *s[1:])
+
+
 try:  # pragma: no cover - exercised only where tensordict is installed
     from tensordict import TensorDict  # type: ignore
 
@@ -36,10 +63,30 @@ except ImportError:  # the stand-in
 
         def __getitem__(self, key):
             if isinstance(key, str):
-                return super().__getitem__(key)
+                v = super().__getitem__(key)
+                if isinstance(v, RepeatedRows):  # first read: make the batchify copy
+                    v = v.materialize()
+                    super().__setitem__(key, v)
+                return v
             out = {k: v[key] for k, v in self.items()}
             ref = torch.empty(self.batch_size, device="meta")[key]
             return TensorDict(out, ref.shape, self._device)
+
+        def __iter__(self):  # keys; also keeps dict(td) off the raw-value fast path
+            return iter(list(super().keys()))
+
+        def items(self):
+            return [(k, self[k]) for k in list(super().keys())]
+
+        def values(self):
+            return [self[k] for k in list(super().keys())]
+
+        def get_raw(self, key, default=None):
+            """The stored entry without materialising a lazy batchify (``RepeatedRows``)."""
+            return super().get(key, default)
+
+        def is_lazy(self, key) -> bool:
+            return isinstance(super().get(key), RepeatedRows)
 
         # -- tensordict-like API -------------------------------------------------
         def set(self, key, value):
@@ -47,10 +94,12 @@ except ImportError:  # the stand-in
             return self
 
         def get(self, key, default=None):
-            return super().get(key, default)
+            return self[key] if key in self else default
 
         def update(self, other, **kw):  # noqa: D401
-            for k, v in dict(other, **kw).items():
+            for k in list(other.keys()):
+                self[k] = other[k]
+            for k, v in kw.items():
                 self[k] = v
             return self
 
@@ -62,8 +111,8 @@ except ImportError:  # the stand-in
         def device(self):
             if self._device is not None:
                 return self._device
-            for v in self.values():
-                if isinstance(v, torch.Tensor):
+            for v in dict.values(self):
+                if isinstance(v, (torch.Tensor, RepeatedRows)):
                     return v.device
             return None
 
@@ -126,5 +175,5 @@ except ImportError:  # the stand-in
             return self._map(lambda v: v.permute(*dims, *range(nb, v.dim())), new)
 
         def __repr__(self):
-            fields = ", ".join(f"{k}: {tuple(v.shape)} {v.dtype}" for k, v in self.items())
+            fields = ", ".join(f"{k}: {tuple(v.shape)}" for k, v in dict.items(self))
             return f"TensorDict({{{fields}}}, batch_size={tuple(self.batch_size)}, device={self.device})"

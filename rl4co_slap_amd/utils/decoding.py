@@ -68,12 +68,18 @@ def process_logits(logits, mask=None, temperature: float = 1.0, top_p: float = 0
 
 
 def get_log_likelihood(logprobs, actions=None, mask=None, return_sum: bool = True):
-    """``decoding.py:39-65``."""
+    """``decoding.py:39-65``.  The ``> -1000`` assert needs a host sync; for logprobs
+    that ``post_decoder_hook`` produced, the same test was folded into its single
+    status read (``_co_logp_ok``), so no second sync happens here."""
+    checked = getattr(logprobs, "_co_logp_ok", None)
     if actions is not None and logprobs.dim() == 3:
         logprobs = logprobs.gather(-1, actions.unsqueeze(-1)).squeeze(-1)
     if mask is not None:
         logprobs[~mask] = 0
-    assert (logprobs > -1000).data.all(), "Logprobs should not be -inf, check sampling procedure!"
+        checked = None  # the precomputed test saw the unmasked values
+    if checked is None:
+        checked = bool((logprobs > -1000).data.all())
+    assert checked, "Logprobs should not be -inf, check sampling procedure!"
     return logprobs.sum(1) if return_sum else logprobs
 
 
@@ -88,7 +94,8 @@ def rollout(env, td, policy, max_steps: int = None):
     """``decoding.py:88-109``."""
     max_steps = float("inf") if max_steps is None else max_steps
     actions, steps = [], 0
-    while not td["done"].all():
+    lb = env.min_steps_to_done(td) if hasattr(env, "min_steps_to_done") else 0
+    while steps < lb or not td["done"].all():  # same stop; polls only once it can be done
         td = policy(td)
         actions.append(td["action"])
         td = env.step(td)["next"]
@@ -149,10 +156,22 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         """``decoding.py:315-325`` + the deferred feasibility assertion."""
         assert len(self.logprobs) > 0, \
             "No logprobs were collected because all environments were done. Check your initial state"
-        if self._status is not None and int(self._status.item()) & nat.ST_INFEASIBLE:
-            raise AssertionError("infeasible action selected")
         logprobs = torch.stack(self.logprobs, 1)
         actions = torch.stack(self.actions, 1)
+        # one host read for the deferred feasibility assert and get_log_likelihood's
+        # `> -1000` test (decoding.py:57-58) on the same logprobs
+        # (per-step selected logprobs only: full [B, steps, N] ones hold -inf at masked
+        # entries, and get_log_likelihood tests them after its gather)
+        flat = logprobs.dim() == 2
+        ok = ((logprobs > -1000).all() if flat else torch.ones((), dtype=torch.bool,
+                                                                device=logprobs.device))
+        ok = ok.to(torch.int32)
+        st = self._status if self._status is not None else torch.zeros_like(ok)
+        st_bits, lp_ok = (int(v) for v in torch.stack([st.reshape(()), ok]).tolist())
+        if st_bits & nat.ST_INFEASIBLE:
+            raise AssertionError("infeasible action selected")
+        if flat:
+            logprobs._co_logp_ok = bool(lp_ok)
         if self.num_starts > 0 and self.select_best:
             logprobs, actions, td, env = self._select_best(logprobs, actions, td, env)
         return logprobs, actions, td, env

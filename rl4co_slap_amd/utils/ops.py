@@ -20,11 +20,33 @@ def _batchify_single(x, repeats: int):
     return x.expand(repeats, *s).contiguous().view(s[0] * repeats, *s[1:])
 
 
+def _batchify_td_lazy(td, repeats: int):
+    """The stand-in TensorDict: every entry becomes a ``RepeatedRows`` (no copy until it
+    is read, see ``td.RepeatedRows``); same keys, shapes and values as the reference's
+    ``expand(...).contiguous().view(...)``."""
+    from ..td import RepeatedRows
+
+    out = TensorDict({}, batch_size=[td.batch_size[0] * repeats, *td.batch_size[1:]])
+    for k in list(td.keys()):
+        v = td.get_raw(k)
+        if isinstance(v, RepeatedRows):  # nested batchify: materialise the inner one
+            v = v.materialize()
+        dict.__setitem__(out, k, RepeatedRows(v, repeats))
+    return out
+
+
 def batchify(x: Union[Tensor, TensorDict], shape):
-    """``ops.py:19-34``: ``b ... -> (r b) ...`` (repeat-major layout)."""
+    """``ops.py:19-34``: ``b ... -> (r b) ...`` (repeat-major layout).  A tensor is
+    copied as in the reference; a (stand-in) TensorDict keeps its entries as lazy
+    ``RepeatedRows`` (zero-copy multistart: the row-index scheme of the POMO episode)."""
     shape = [shape] if isinstance(shape, int) else shape
     for s in reversed(shape):
-        x = _batchify_single(x, s) if s > 0 else x
+        if s <= 0:
+            continue
+        if hasattr(x, "get_raw") and len(x.batch_size) >= 1:
+            x = _batchify_td_lazy(x, s)
+        else:
+            x = _batchify_single(x, s)
     return x
 
 

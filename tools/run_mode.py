@@ -1,6 +1,6 @@
 """Run one bench.py mode alone (for rocprofv3 kernel traces of a single path).
 
-    python tools/run_mode.py cvrp|slap|slap65k|pomo|tsp|gen [--k K]
+    python tools/run_mode.py cvrp|slap|slap65k|pomo|dropin|tsp|gen [--k K]
 """
 import argparse
 import json
@@ -33,6 +33,8 @@ def main():
         out = bench.bench_slap(16384, a.k, 1, 0, dev)
     elif a.mode == "slap65k":
         out = bench.bench_slap(65536, a.k, 1, 0, dev, stepwise=False)
+    elif a.mode == "dropin":
+        out = bench.bench_dropin(65536, 100, a.k, 1, 0, dev)
     elif a.mode == "pomo":
         out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev)
     elif a.mode == "tsp":
