@@ -115,7 +115,15 @@ def ptr(t):
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(t: torch.Tensor):
+    """The current HIP stream of the tensor's device, as a handle (the raw-stream query:
+    ~0.3 us against ~4 us for torch.cuda.current_stream(dev).cuda_stream per call)."""
+    idx = t.device.index
+    if _raw_stream is not None and idx is not None:
+        return _raw_stream(idx)
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
