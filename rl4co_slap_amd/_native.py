@@ -107,6 +107,46 @@ def load():
         return lib
 
 
+HOST_LIB_PATH = os.path.join(_HERE, "_lib", "libco_env_host.so")
+_host = None
+# the host (CPU) library exports the env / decode subset of the C ABI (csrc/host)
+HOST_SYMBOLS = ["co_tsp_reset", "co_tsp_step", "co_tsp_reward", "co_any_eq_i64",
+                "co_cvrp_reset", "co_cvrp_step", "co_cvrp_action_mask", "co_cvrp_reward",
+                "co_slap_reset", "co_slap_step", "co_slap_reward", "co_gather_by_index",
+                "co_decode_step"]
+
+
+class _HostStream:
+    """`stream_of` for a CPU tensor: routes the call to the host library."""
+
+    def __repr__(self):
+        return "HOST"
+
+
+HOST = _HostStream()
+
+
+def load_host():
+    """The host build (TensorDicts on the CPU, BASELINE config 1); raises if missing."""
+    global _host
+    if _host is not None:
+        return _host
+    with _lock:
+        if _host is not None:
+            return _host
+        if not os.path.exists(HOST_LIB_PATH):
+            raise NativeUnavailable(
+                f"rl4co_slap_amd: host library {HOST_LIB_PATH} is missing (CPU TensorDicts); "
+                "build it with `python -m rl4co_slap_amd.csrc.build`.")
+        lib = ctypes.CDLL(HOST_LIB_PATH)
+        for name in HOST_SYMBOLS:
+            fn = getattr(lib, name)
+            fn.argtypes = _SIGS[name]
+            fn.restype = ctypes.c_int
+        _host = lib
+        return lib
+
+
 def exported_symbols():
     return list(_SIGS) + ["co_build_info"]
 
@@ -120,7 +160,10 @@ _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
 def stream_of(t: torch.Tensor):
     """The current HIP stream of the tensor's device, as a handle (the raw-stream query:
-    ~0.3 us against ~4 us for torch.cuda.current_stream(dev).cuda_stream per call)."""
+    ~0.3 us against ~4 us for torch.cuda.current_stream(dev).cuda_stream per call); for a
+    CPU tensor the HOST marker (the call goes to the host library)."""
+    if t.device.type == "cpu":
+        return HOST
     idx = t.device.index
     if _raw_stream is not None and idx is not None:
         return _raw_stream(idx)
@@ -128,15 +171,28 @@ def stream_of(t: torch.Tensor):
 
 
 def require_device(*tensors):
-    for t in tensors:
-        if t is not None and t.device.type != "cuda":
-            raise RuntimeError(
-                "rl4co_slap_amd runs the env on the HIP device only (no CPU fallback); "
-                f"got a tensor on {t.device}. Move the TensorDict with td.to('cuda').")
+    """All tensors on the HIP device, or all on the CPU (the host build; the caller's
+    C-ABI call then goes to libco_env_host.so).  Mixed devices raise."""
+    devs = {t.device.type for t in tensors if t is not None}
+    if devs <= {"cuda"}:
+        return
+    if devs == {"cpu"}:
+        load_host()  # raises when the host library was not built
+        return
+    raise RuntimeError(f"rl4co_slap_amd: tensors on mixed devices {sorted(devs)}; the env "
+                       "runs on the HIP device or, for CPU TensorDicts, the host build")
 
 
 def call(name, *args):
-    rc = getattr(load(), name)(*args)
+    if args and args[-1] is HOST:
+        lib = load_host()
+        if name not in HOST_SYMBOLS:
+            raise NotImplementedError(f"{name} has no host (CPU) build; move the TensorDict "
+                                      "to the HIP device")
+        args = args[:-1] + (None,)
+    else:
+        lib = load()
+    rc = getattr(lib, name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with status {rc}")
 

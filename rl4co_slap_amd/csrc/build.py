@@ -46,6 +46,8 @@ def build(force=False, verbose: bool = False) -> str:
     from concurrent.futures import ThreadPoolExecutor
 
     if not force and not _stale():
+        if not os.path.exists(HOST_LIB) or os.path.getmtime(HOST_LIB) < os.path.getmtime(HOST_SRC):
+            build_host(verbose=verbose)
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     obj_dir = os.path.join(OUT_DIR, "obj")
@@ -78,7 +80,27 @@ def build(force=False, verbose: bool = False) -> str:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    build_host(verbose=verbose)
     return LIB
+
+
+HOST_SRC = os.path.join(HERE, "host", "co_env_host.cpp")
+HOST_LIB = os.path.join(OUT_DIR, "libco_env_host.so")
+HOST_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+              "-Wall", "-Wextra"]
+
+
+def build_host(verbose: bool = False, out: str = HOST_LIB, extra=()) -> str:
+    """The host (CPU) build of the env / decode entry points (csrc/host): g++, the same
+    C ABI, for TensorDicts on the CPU.  ``extra`` adds flags (the sanitizer build)."""
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [cxx] + HOST_FLAGS + list(extra) + ["-o", out + ".tmp", HOST_SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

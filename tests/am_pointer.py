@@ -1,0 +1,84 @@
+"""An AM-shaped pointer decoder for the drop-in tests (test helper, not product code):
+``am/decoder.py:162-200`` (query from the context embedding, multi-head glimpse over the
+node embeddings under ``action_mask``, single-head pointer logits) with the TSP context of
+``context.py:102-137`` (first + current node embeddings, a learned placeholder at
+``i == 0``).  It reads ``first_node`` / ``current_node`` / ``i`` / ``action_mask`` from the
+env's TensorDict exactly as the AM does.  ``oracle_logits_fn`` evaluates the same network
+from the oracle's own state (on ``dev``), so identical states give identical logits."""
+import math
+
+import torch
+from torch import nn
+
+H, HEADS = 32, 4
+
+
+class PointerDecoder(nn.Module):
+    """A small attention-model decoder (random init, eval mode, on the device)."""
+
+    def __init__(self, locs_bn2, dev, depot_env=False):
+        super().__init__()
+        g = torch.Generator().manual_seed(5)
+
+        def lin(i, o):
+            m = nn.Linear(i, o, bias=False)
+            with torch.no_grad():
+                m.weight.copy_(torch.randn(o, i, generator=g) / math.sqrt(i))
+            return m
+
+        self.init_embed = lin(2, H)
+        self.wq, self.wk, self.wv, self.wo, self.wl = (lin(2 * H, H), lin(H, H), lin(H, H),
+                                                       lin(H, H), lin(H, H))
+        self.placeholder = nn.Parameter(torch.randn(2 * H, generator=g))
+        self.depot_env = depot_env
+        self.to(dev).eval()
+        with torch.no_grad():  # "encoder": node embeddings of the B instances
+            self.h = self.init_embed(locs_bn2.to(dev))
+        self.b = locs_bn2.shape[0]
+
+    @torch.no_grad()
+    def logits(self, first, cur, i, mask):
+        """am/decoder.py:162-200 shaped: glimpse + pointer; rows e of a multistart batch
+        use instance e % B's embeddings (the AM batchifies its cached embeddings)."""
+        e = first.shape[0]
+        h = self.h[torch.arange(e, device=self.h.device) % self.b]  # [E, N, H]
+        n = h.shape[1]
+        hf = h.gather(1, first.reshape(e, 1, 1).expand(e, 1, H)).squeeze(1)
+        hc = h.gather(1, cur.reshape(e, 1, 1).expand(e, 1, H)).squeeze(1)
+        ctx = torch.cat([hf, hc], -1)
+        if not self.depot_env:  # TSP context: the placeholder before the first step
+            ctx = torch.where((i.reshape(e, 1) == 0), self.placeholder.expand(e, -1), ctx)
+        q = self.wq(ctx).view(e, HEADS, 1, H // HEADS)
+        k = self.wk(h).view(e, n, HEADS, H // HEADS).transpose(1, 2)
+        v = self.wv(h).view(e, n, HEADS, H // HEADS).transpose(1, 2)
+        att = (q @ k.transpose(-1, -2)) / math.sqrt(H // HEADS)
+        att = att.masked_fill(~mask.view(e, 1, 1, n), float("-inf"))
+        glimpse = self.wo((att.softmax(-1) @ v).reshape(e, H))
+        return (glimpse.unsqueeze(1) @ self.wl(h).transpose(1, 2)).squeeze(1) / math.sqrt(H)
+
+    # ConstructiveDecoder interface (constructive/base.py:43-86)
+    def forward(self, td, hidden=None, num_starts: int = 0):
+        first = td["first_node"] if not self.depot_env else td["current_node"]
+        i = td["i"] if "i" in td else torch.ones_like(td["current_node"])
+        return self.logits(first, td["current_node"], i, td["action_mask"]), td["action_mask"]
+
+    def pre_decoder_hook(self, td, env, hidden=None, num_starts: int = 0):
+        return td, env, hidden
+
+
+def _oracle_logits_fn(dec, dev):
+    def fn(td):  # the same network on the device, from the ORACLE's state
+        first = td["first_node"] if not dec.depot_env else td["current_node"]
+        i = td["i"] if "i" in td.keys() else torch.ones_like(td["current_node"])
+        return dec.logits(first.to(dev), td["current_node"].to(dev), i.to(dev),
+                          td["action_mask"].to(dev)).cpu()
+    return fn
+
+
+def oracle_logits_fn(dec, dev):
+    def fn(td):  # the same network on `dev`, from the ORACLE's state
+        first = td["first_node"] if not dec.depot_env else td["current_node"]
+        i = td["i"] if "i" in td.keys() else torch.ones_like(td["current_node"])
+        return dec.logits(first.to(dev), td["current_node"].to(dev), i.to(dev),
+                          td["action_mask"].to(dev)).cpu()
+    return fn

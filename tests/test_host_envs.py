@@ -1,0 +1,161 @@
+"""The host (CPU) build of the env / decode entry points (csrc/host/co_env_host.cpp,
+libco_env_host.so) driven through the same env classes on CPU TensorDicts -- BASELINE
+config 1, the reference's CPU TensorDict path (``tsp/env.py:95-120`` allocates on
+``td.device``) -- against the oracle on identical seeded instances and actions.
+
+Bar as on the device: masks / indices / bool and int state and CVRP capacity floats
+bit-exact, decode log-probabilities bit-exact with ATen's F.log_softmax (the host build
+restates SLEEF expf/logf and map_reduce_all's order), rewards within 1e-5.  CPU only
+(no GPU marker): these run in the driver's CPU suite."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.decoding import process_logits as ref_process_logits
+from oracle.decoding import tanh_cr
+from oracle.envs import (CVRPOracle, SLAPOracle, TSPOracle, cvrp_nearest_action,
+                         slap_closest_free_action)
+from oracle.rollout import constructive_forward
+from oracle.rollout import rollout as ref_rollout
+from oracle.td import TD
+from rl4co_slap_amd import TensorDict
+from rl4co_slap_amd import _native as nat
+from rl4co_slap_amd.envs import CVRPEnv, SLAPEnv, TSPEnv
+from rl4co_slap_amd.rollout import ConstructivePolicy
+from rl4co_slap_amd.utils.decoding import decode_step
+from rl4co_slap_amd.utils.decoding import rollout as host_rollout
+
+from am_pointer import PointerDecoder, oracle_logits_fn
+
+CPU = torch.device("cpu")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def host_lib():
+    import os
+
+    from rl4co_slap_amd.csrc.build import HOST_LIB, build_host
+
+    if not os.path.exists(HOST_LIB):
+        build_host()
+    nat.load_host()
+
+
+def _close(got, want):
+    assert ((got - want).abs() <= 1e-5 * want.abs().clamp(min=1)).all(), (got - want).abs().max()
+
+
+@pytest.mark.parametrize("b,n", [(1, 5), (128, 20), (33, 100)])
+def test_tsp_cpu_episode_every_step(b, n):
+    ref_env = TSPOracle(num_loc=n, seed=3)
+    td_ref = ref_env.reset(batch_size=[b])
+    env = TSPEnv(generator_params=dict(num_loc=n), device="cpu")
+    td = env.reset(TensorDict({"locs": td_ref["locs"].clone()}, [b]))
+    assert td["action_mask"].device == CPU
+    acts = torch.rand(b, n, generator=torch.Generator().manual_seed(7)).argsort(1)
+    for t in range(n):
+        td_ref["action"] = acts[:, t].clone()
+        td_ref = ref_env.step(td_ref)["next"]
+        td["action"] = acts[:, t].clone()
+        td = env.step(td)["next"]
+        for k in ("action_mask", "first_node", "current_node", "i", "done", "reward"):
+            assert torch.equal(td[k], td_ref[k]), (k, t)
+    _close(env.get_reward(td, acts), ref_env.get_reward(td_ref, acts))
+    bad = acts.clone()
+    bad[0, 1] = bad[0, 0]
+    with pytest.raises(AssertionError, match="Invalid tour"):
+        env.get_reward(td, bad)
+
+
+def test_cvrp_cpu_nearest_episode():
+    b, n = 40, 20
+    ref_env = CVRPOracle(num_loc=n, seed=5)
+    gen = ref_env.generate([b])
+    env = CVRPEnv(generator_params=dict(num_loc=n), device="cpu")
+    td_ref = ref_env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    td = env.reset(TensorDict({k: v.clone() for k, v in gen.items()}, [b]))
+    acts = []
+    while not td_ref["done"].all():
+        a = cvrp_nearest_action(td_ref)
+        acts.append(a)
+        td_ref["action"] = a
+        td_ref = ref_env.step(td_ref)["next"]
+        td["action"] = a.clone()
+        td = env.step(td)["next"]
+        for k in ("action_mask", "visited", "used_capacity", "current_node", "done"):
+            assert torch.equal(td[k], td_ref[k]), k
+    acts = torch.stack(acts, 1)
+    _close(env.get_reward(td, acts), ref_env.get_reward(td_ref, acts))
+    over = acts.clone()
+    over[:, :] = 0
+    with pytest.raises(AssertionError, match="Invalid tour"):
+        env.get_reward(td, over)
+
+
+def test_slap_cpu_closest_episode():
+    b = 24
+    ref_env = SLAPOracle(seed=9)
+    np.random.seed(9)
+    gen = ref_env.generate([b])
+    td_ref = ref_env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    env = SLAPEnv(device="cpu")
+    td = env.reset(TensorDict({k: v.clone() for k, v in gen.items()}, [b]))
+    r_ref, tdf, a = ref_rollout(ref_env, td_ref, slap_closest_free_action)
+    it = iter(range(a.shape[1]))
+    r, tdh, ah = host_rollout(env, td, lambda t: t.set("action", a[:, next(it)].clone()))
+    assert torch.equal(ah, a)
+    for k in ("action_mask", "i", "assignment", "done"):
+        assert torch.equal(tdh[k], tdf[k]), k
+    _close(r, r_ref)
+
+
+@pytest.mark.parametrize("clip", [0.0, 10.0])
+@pytest.mark.parametrize("temp", [1.0, 0.7])
+@pytest.mark.parametrize("n", [7, 20, 100])
+def test_decode_step_cpu_bit_exact(clip, temp, n):
+    b = 64
+    g = torch.Generator().manual_seed(n)
+    logits = torch.randn(b, n, generator=g) * 3
+    logits[5, :] = logits[5, 0]  # an exact tie row
+    mask = torch.rand(b, n, generator=g) > 0.3
+    mask[:, 0] = True
+    want = ref_process_logits(logits, mask, temp, clip, tanh=tanh_cr)
+    act, lp, full = decode_step(logits, mask, "greedy", temp, clip, return_full=True)
+    assert torch.equal(full, want)
+    assert torch.equal(act, want.argmax(-1))
+    assert torch.equal(lp, want.gather(1, act[:, None]).squeeze(1))
+    ev = torch.randint(0, n, (b,), generator=g)
+    _, lpe, _ = decode_step(logits, None, "evaluate", temp, clip, action=ev)
+    w2 = ref_process_logits(logits, None, temp, clip, tanh=tanh_cr, mask_logits=False)
+    assert torch.equal(lpe, w2.gather(1, ev[:, None]).squeeze(1))
+
+
+@pytest.mark.parametrize("decode_type", ["greedy", "multistart_greedy"])
+def test_config1_tsp20_am_greedy_on_cpu(decode_type):
+    """BASELINE config 1: TSP-20, B=128, AM-shaped greedy rollout on the CPU TensorDict
+    path -- the pointer network evaluated on the CPU from each loop's own state."""
+    b, n = 128, 20
+    ref_env = TSPOracle(num_loc=n, seed=1234)
+    gen = ref_env.generate([b])
+    td_ref = ref_env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    env = TSPEnv(generator_params=dict(num_loc=n), device="cpu")
+    td = env.reset(TensorDict({"locs": gen["locs"].clone()}, [b]))
+    dec = PointerDecoder(gen["locs"], CPU)
+    ref = constructive_forward(td_ref, ref_env, oracle_logits_fn(dec, CPU),
+                               decode_type=decode_type, tanh_clipping=10.0)
+    pol = ConstructivePolicy(None, dec, env_name="tsp", tanh_clipping=10.0)
+    out = pol(td, env, phase="test", decode_type=decode_type, return_actions=True)
+    assert torch.equal(out["actions"], ref["actions"])
+    _close(out["reward"], ref["reward"])
+    _close(out["log_likelihood"], ref["log_likelihood"])
+
+
+def test_mixed_devices_and_missing_host_symbols_raise():
+    env = TSPEnv(generator_params=dict(num_loc=5), device="cpu")
+    td = env.reset(batch_size=[3])
+    with pytest.raises(NotImplementedError, match="no host"):
+        decode_step(torch.zeros(3, 5), None, "greedy", top_k=2)
+    if torch.cuda.is_available():
+        td["action"] = torch.zeros(3, dtype=torch.int64, device="cuda")
+        with pytest.raises(RuntimeError, match="mixed devices"):
+            env.step(td)
