@@ -77,9 +77,15 @@ def test_registry():
         get_env("ffsp")
 
 
-def test_product_refuses_cpu_tensors():
+def test_cpu_tensors_need_the_host_build(monkeypatch):
+    """CPU TensorDicts run on the host build of the C ABI (libco_env_host.so), never on a
+    Python/oracle fallback: without that library they raise."""
+    from rl4co_slap_amd import _native as nat
+
+    monkeypatch.setattr(nat, "HOST_LIB_PATH", "/nonexistent/libco_env_host.so")
+    monkeypatch.setattr(nat, "_host", None)
     env = TSPEnv(generator_params=dict(num_loc=5), device="cpu")
-    with pytest.raises(RuntimeError, match="HIP device"):
+    with pytest.raises(nat.NativeUnavailable, match="host library"):
         env.reset(batch_size=[2])
 
 
