@@ -484,6 +484,9 @@ def main():
         # the same with the opt-in CO_DECODE_FAST math (not bit-exact; reported separately)
         modes["pomo_tsp100_fast_math"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev,
                                                     fast_math=True)
+        # certified greedy: exact actions at close to the fast-math speed
+        modes["pomo_tsp100_certified"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev,
+                                                    certified=True)
         # CVRP-100 (config 3), nearest-feasible policy: fused episode and stepwise loop
         modes.update(bench_cvrp(32768, 100, k, world, rank, dev))
         # instance generation, timed separately (SURVEY.md 8d protocol; 8f rank 1)
@@ -567,6 +570,7 @@ def annotate_modes(modes, n, world):
         "slap_stepwise_graph_teacher": lambda m: 234 + 1684 / 20,
         "pomo_tsp100": lambda m: 6 * n + 54,
         "pomo_tsp100_fast_math": lambda m: 6 * n + 54,
+        "pomo_tsp100_certified": lambda m: 6 * n + 54,
         "cvrp_fused_nearest": lambda m: (8 + 12 * n + 8 * m["episode_steps"] + 10 * (n + 1) + 25)
         / m["episode_steps"],
         "cvrp_stepwise_graph": lambda m: 7 * n + 33 + (16 * m["episode_steps"] + 12)
@@ -823,7 +827,7 @@ def bench_generate_uniform(b, n, dev, reps=5):
     return out
 
 
-def bench_pomo(b, n, k, world, rank, dev, fast_math=False):
+def bench_pomo(b, n, k, world, rank, dev, fast_math=False, certified=False):
     from rl4co_slap_amd.rollout.pomo import POMOEpisode, global_metrics
 
     torch.manual_seed(1234 + rank)
@@ -831,7 +835,8 @@ def bench_pomo(b, n, k, world, rank, dev, fast_math=False):
     e = b * n
     g = torch.Generator(device=dev).manual_seed(99 + rank)
     logits = torch.randn((n - 1, e, n), generator=g, device=dev)  # policy-network stand-in
-    ep = POMOEpisode(locs, logits, tanh_clipping=10.0, fast_math=fast_math).capture()
+    ep = POMOEpisode(locs, logits, tanh_clipping=10.0, fast_math=fast_math,
+                     certified=certified).capture()
 
     def run():
         ep.replay()
@@ -853,7 +858,10 @@ def bench_pomo(b, n, k, world, rank, dev, fast_math=False):
             "instances_per_gpu": b, "starts": n, "envs_per_gpu": e,
             "bytes_per_env_step_decode_fused": 6 * n + 54,
             "decode_math": "fast (CO_DECODE_FAST, opt-in, not bit-exact)" if fast_math
-            else "exact (ATen log_softmax bits, correctly rounded tanh)",
+            else ("certified (CO_DECODE_CERTIFIED: greedy actions = the exact path's by a "
+                  "per-row error bound + exact recomputation of uncertified waves; logp fast, "
+                  "within ~1e-6)" if certified
+                  else "exact (ATen log_softmax bits, correctly rounded tanh)"),
             "allgather_ms": t_ag * 1e3,
             "allgather_note": "median of 10 after a warm-up call" + (
                 "" if world > 1 else "; world size 1: no collective runs, host bookkeeping only"),

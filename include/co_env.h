@@ -169,6 +169,12 @@ int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t* flag, voi
  * logits (SLEEF expf/logf and vec::map_reduce_all's 16-lane order), tanh correctly
  * rounded; with it logp is within ~1e-6 and greedy picks may differ on near-ties. */
 #define CO_DECODE_FAST 0x100
+/* mode flag, opt-in: greedy picks computed with the fast math and certified per row by
+ * its error bound (the runner-up must trail the pick by more than the fast tanh error
+ * times the clip plus two ulps of the log-sum-exp); any wave holding an uncertified row
+ * is recomputed with the exact math.  Greedy actions are therefore the exact path's;
+ * the selected logp is the fast one (within ~1e-6).  Other modes run exact under it. */
+#define CO_DECODE_CERTIFIED 0x200
 
 /* DecodingStrategy.step (rl4co/utils/decoding.py:141-191,327-399,489-499):
  * x = logits[b*logits_stride + c]; tanh clip (tanh_clipping > 0); masked

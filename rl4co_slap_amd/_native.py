@@ -71,6 +71,7 @@ ST_INFEASIBLE = 4
 ST_INDEX_RANGE = 8
 ST_TRUNCATED = 16
 DECODE_FAST = 0x100  # CO_DECODE_FAST mode flag (opt-in fast math; not bit-exact)
+DECODE_CERTIFIED = 0x200  # CO_DECODE_CERTIFIED: fast math, greedy actions certified exact
 
 _lock = threading.Lock()
 _lib = None

@@ -32,6 +32,7 @@ using namespace co;
 #ifndef CO_DECODE_UNR
 #define CO_DECODE_UNR 1
 #endif
+
 #if defined(CO_DIAG_FASTTANH) || defined(CO_DIAG_FASTEXP)
 // timing-diagnostic build: the "exact" decode is not exact (see _native.load())
 extern "C" __attribute__((visibility("default"))) const int co_variant_timing_cut_decode = 1;
@@ -48,8 +49,10 @@ __device__ __forceinline__ float co_tanh_fast(float x) {
 __device__ __forceinline__ float co_exp_fast(float x) { return co_exp2(x * 1.4426950408889634f); }
 
 // OPT template flags of the row engines: bit 0 tanh clipping, bit 1 temperature != 1,
-// bit 2 the fast math above (default: ATen-exact, co_math.hpp)
-constexpr int kOptClip = 1, kOptTemp = 2, kOptFast = 4;
+// bit 2 the fast math above (default: ATen-exact, co_math.hpp), bit 3 certified greedy
+// (GreedyRow kernels only, CO_DECODE_CERTIFIED: fast math, then the exact recomputation
+// for every wave holding a row whose fast argmax the error bound cannot certify)
+constexpr int kOptClip = 1, kOptTemp = 2, kOptFast = 4, kOptCert = 8;
 
 template <int OPT>
 __device__ __forceinline__ float clip_tanh(float x) {
@@ -449,6 +452,36 @@ struct GreedyRow {
     return row_log_sum_exp<RL, EPL, OPT>(v, N, sl, lds_row);
   }
 
+  // CO_DECODE_CERTIFIED: after softmax_shift with the fast math (v[k] = z'_k - m', L' the
+  // fast log-sum-exp) and select (sel), is `sel` provably the exact path's greedy action?
+  // The exact action is the first index of max fl(fl(z_k - m) - L) (z: the clipped /
+  // masked / scaled logits the exact path computes).  Certified when the fast runner-up
+  // trails the selected value by more than
+  //   2 eps_z / T            (|z'_k - z_k| <= eps_z: fast tanh abs error <= 1.5e-6, times
+  //                          the clip, plus the roundings of the product; 0 without clip)
+  //   + 2 ulp bound of L     (then fl(d_k - L) < fl(0 - L) for every k != sel: no rounding
+  //                          tie with the maximum)
+  // and L' is finite.  Non-finite rows (all masked, NaN / inf logits) are never certified.
+  template <int OPT>
+  __device__ __forceinline__ bool certify(float L, int sel, int c0, int N, float clip,
+                                          float temp) const {
+    float ru = -__builtin_inff();
+#pragma unroll
+    for (int k = 0; k < EPL; ++k)
+      if (c0 + k < N && c0 + k != sel) ru = fmaxf(ru, v[k]);  // masked entries are -inf
+    ru = grp_max<RL>(ru);
+    int e;
+    frexpf(fabsf(L) + 1.f, &e);               // |L| + 1 < 2^e: ulp(L) <= 2^(e - 24)
+    float delta = ldexpf(1.f, e - 22) + 1e-7f;  // 2 x (2 ulp), margin included
+    if (OPT & kOptClip) {
+      int ec;
+      frexpf(clip, &ec);
+      const float ez = clip * 1.5e-6f + ldexpf(3.f, ec - 24);
+      delta += 2.f * ((OPT & kOptTemp) ? ez / temp : ez);
+    }
+    return __builtin_isfinite(L) && -ru > delta;  // ru NaN -> false
+  }
+
   // greedy action of the row (valid on every lane of the group) and its logp
   __device__ __forceinline__ int select(float L, int c0, float& lp) const {
     lp = 0.f - L;
@@ -459,6 +492,35 @@ struct GreedyRow {
     return idx == 0x7fffffff ? 0 : idx;  // no match only when L is NaN: all logp NaN
   }
 };
+
+// One row's greedy step on the GreedyRow engine: softmax_shift + select, or, with
+// kOptCert, the fast math certified per row and the exact math for any wave that holds an
+// uncertified valid row (wave-uniform branch: the group reductions need every lane).
+// Returns the action; L and lp as select().
+template <int OPT, int RL, int EPL, int VW>
+__device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid, int N, float clip,
+                                          float temp, int sl, int c0, float* lds_row, float& L,
+                                          float& lp) {
+  if constexpr ((OPT & kOptCert) != 0) {
+    constexpr int OF = (OPT & ~kOptCert) | kOptFast, OE = OPT & ~(kOptCert | kOptFast);
+    float raw[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) raw[k] = g.v[k];
+    L = g.template softmax_shift<OF>(clip, temp, N, sl, lds_row);
+    int sel = g.select(L, c0, lp);
+    const bool ok = !valid || g.template certify<OF>(L, sel, c0, N, clip, temp);
+    if (__any(!ok)) {  // rare: the exact evaluation for the whole wave
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) g.v[k] = raw[k];
+      L = g.template softmax_shift<OE>(clip, temp, N, sl, lds_row);
+      sel = g.select(L, c0, lp);
+    }
+    return sel;
+  } else {
+    L = g.template softmax_shift<OPT>(clip, temp, N, sl, lds_row);
+    return g.select(L, c0, lp);
+  }
+}
 
 template <int RL, int EPL, int VW, int OPT>
 __global__ __launch_bounds__(256) void decode_greedy_kernel(
@@ -476,9 +538,9 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
     const int64_t r = valid ? row : 0;
     GreedyRow<RL, EPL, VW> g;
     g.load(valid, N, logits + r * lstride, mask ? mask + r * (int64_t)N : nullptr, c0);
-    const float L = g.template softmax_shift<OPT>(clip, temp, N, sl, group_scratch<RL, EPL>(lds, grp));
-    float lp;
-    const int sel = g.select(L, c0, lp);
+    float lp, L;
+    const int sel = greedy_row<OPT>(g, valid, N, clip, temp, sl, c0, group_scratch<RL, EPL>(lds, grp),
+                                    L, lp);
     if (!valid) continue;
     if (full) g.store_logp(N, L, full + r * (int64_t)N, c0);
     if (sl == 0) {
@@ -640,9 +702,9 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     }
     GreedyRow<RL, EPL, VW> g;
     g.load(valid, N, logits + r * lstride, mask_in + r * (int64_t)N, c0);
-    const float L = g.template softmax_shift<OPT>(clip, temp, N, sl, group_scratch<RL, EPL>(lds, grp));
-    float lp;
-    const int sel = g.select(L, c0, lp);
+    float lp, L;
+    const int sel = greedy_row<OPT>(g, valid, N, clip, temp, sl, c0, group_scratch<RL, EPL>(lds, grp),
+                                    L, lp);
     const bool feas0 = g.allowed(0);
     uint32_t left = 0u;
 #pragma unroll
@@ -699,6 +761,22 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     }                                                                                   \
   } while (0)
 
+// greedy kernels: the same eight, or (cert) the four certified variants
+#define CO_OPT_DISPATCH_G(LAUNCH, KERNEL, ...)                                          \
+  do {                                                                                  \
+    const int opt_ = (clip > 0.f ? kOptClip : 0) | (temp != 1.f ? kOptTemp : 0);        \
+    if (cert) {                                                                         \
+      switch (opt_ | kOptCert) {                                                        \
+        CO_OPT_CASE(8, LAUNCH, KERNEL, __VA_ARGS__)                                     \
+        CO_OPT_CASE(9, LAUNCH, KERNEL, __VA_ARGS__)                                     \
+        CO_OPT_CASE(10, LAUNCH, KERNEL, __VA_ARGS__)                                    \
+        CO_OPT_CASE(11, LAUNCH, KERNEL, __VA_ARGS__)                                    \
+      }                                                                                 \
+    } else {                                                                            \
+      CO_OPT_DISPATCH(LAUNCH, KERNEL, __VA_ARGS__);                                     \
+    }                                                                                   \
+  } while (0)
+
 inline unsigned decode_grid(int64_t B, int N, int unr = 1) {
   const int rl = N <= 16 ? CO_RL16 : N <= 32 ? CO_RL32 : N <= 64 ? CO_RL64
                : N <= 128 ? CO_RL128 : N <= 256 ? CO_RL256 : 64;
@@ -730,8 +808,11 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
                                  uint64_t offset, int32_t* status, void* stream) {
   if (B < 0 || N <= 0 || N > 64 * 32 || top_k < 0 || top_p < 0.0 || top_p > 1.0)
     return CO_E_INVAL;
+  // CO_DECODE_CERTIFIED changes only greedy picks' math (actions stay exact); other modes
+  // and the filtered path run the exact math under it
+  const bool cert = (mode & CO_DECODE_CERTIFIED) != 0 && (mode & CO_DECODE_FAST) == 0;
   const bool fast = (mode & CO_DECODE_FAST) != 0;
-  mode &= ~CO_DECODE_FAST;
+  mode &= ~(CO_DECODE_FAST | CO_DECODE_CERTIFIED);
   if (mode < 0 || mode > 2) return CO_E_MODE;
   if (B == 0) return CO_OK;
   if (!logits || !action_out) return CO_E_INVAL;
@@ -741,7 +822,7 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
   const bool filtered = (top_k > 0 && top_k < N) || (top_p > 0.0 && top_p < 1.0);
   if (mode == CO_DECODE_GREEDY && !filtered) {
 #define CO_GREEDY(RL, EPL, V)                                                                  \
-  CO_OPT_DISPATCH(hipLaunchKernelGGL, (decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>),  \
+  CO_OPT_DISPATCH_G(hipLaunchKernelGGL, (decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), \
                   grid, block, 0, s, B, (int)N, logits, lstride, mask, clip, temp, action_out,  \
                   logp_sel, full, status)
     switch (greedy_vw(N, lstride, logits, mask, mask, full)) {
@@ -783,8 +864,9 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
                                   uint8_t* done, uint8_t* step_reward, float* ll_accum,
                                   int32_t* status, void* stream) {
   if (B < 0 || N <= 0 || N > 64 * 32) return CO_E_INVAL;
+  const bool cert = (mode & CO_DECODE_CERTIFIED) != 0 && (mode & CO_DECODE_FAST) == 0;
   const bool fast = (mode & CO_DECODE_FAST) != 0;
-  mode &= ~CO_DECODE_FAST;
+  mode &= ~(CO_DECODE_FAST | CO_DECODE_CERTIFIED);
   if (mode < 0 || mode > 2 || first_mode < 0 || first_mode > 1) return CO_E_MODE;
   if (B == 0) return CO_OK;
   if (!logits || !mask_in || !action_out || !mask_out || !i_in || !i_out || !first_out ||
@@ -795,8 +877,8 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
   if (mode == CO_DECODE_GREEDY) {
     const dim3 grid(decode_grid(B, (int)N)), block(256);
 #define CO_TDG(RL, EPL, V)                                                                     \
-  CO_OPT_DISPATCH(hipLaunchKernelGGL,                                                          \
-                  (tsp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), grid, block, 0, \
+  CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \
+                    (tsp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), grid, block, 0, \
                   s, B, (int)N, logits, lstride, mask_in, clip, temp, action_out, logp_sel,     \
                   mask_out, i_in, i_out, first_in, first_out, first_mode, done, step_reward,    \
                   ll_accum, status)

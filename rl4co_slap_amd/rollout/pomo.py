@@ -33,7 +33,8 @@ from .engine import _GraphEpisode
 
 class POMOEpisode(_GraphEpisode):
     def __init__(self, locs: torch.Tensor, logits: torch.Tensor, num_starts: int = None,
-                 tanh_clipping: float = 10.0, check: bool = True, fast_math: bool = False):
+                 tanh_clipping: float = 10.0, check: bool = True, fast_math: bool = False,
+                 certified: bool = False):
         super().__init__(locs.device)
         b, n, _ = locs.shape
         s = n if num_starts is None else num_starts
@@ -42,8 +43,9 @@ class POMOEpisode(_GraphEpisode):
         d = locs.device
         self.b, self.n, self.s, self.e = b, n, s, e
         self.clip, self.check = float(tanh_clipping), check
-        # fast_math: CO_DECODE_FAST (opt-in; log-probs within ~1e-6, not bit-exact)
-        self.mode = nat.DECODE_FAST if fast_math else 0
+        # fast_math: CO_DECODE_FAST (opt-in; log-probs within ~1e-6, not bit-exact);
+        # certified: CO_DECODE_CERTIFIED (greedy actions = the exact path's, log-probs fast)
+        self.mode = nat.DECODE_FAST if fast_math else (nat.DECODE_CERTIFIED if certified else 0)
         self.locs, self.logits = locs.contiguous(), logits.contiguous()
         self.acts = torch.empty((n, e), dtype=torch.int64, device=d)
         self.acts[0] = torch.arange(s, device=d).repeat_interleave(b) % n  # ops.py:150-154

@@ -37,6 +37,8 @@ def main():
         out = bench.bench_dropin(65536, 100, a.k, 1, 0, dev)
     elif a.mode == "pomo":
         out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev)
+    elif a.mode == "pomo_cert":
+        out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev, certified=True)
     elif a.mode == "tsp":
         from rl4co_slap_amd.rollout.engine import TSPFusedEpisode
 
