@@ -184,16 +184,59 @@ def require_device(*tensors):
                        "runs on the HIP device or, for CPU TensorDicts, the host build")
 
 
+_KIND = {_i64: "i", _i32: "i", _u64: "i", _p: "i", _f32: "f", _f64: "d"}
+_fast = None  # (invoke, {name: (address, kinds)}, {name: (address, kinds)}) once loaded
+FASTCALL_PATH = os.path.join(_HERE, "_lib", "_co_fastcall.so")
+
+
+def _fastcall():
+    """The CPython fast-call module (csrc/pycall/co_fastcall.cpp) with the entry points'
+    addresses and argument classes, or None (then ctypes is used)."""
+    global _fast
+    if _fast is not None:
+        return _fast or None
+    _fast = False
+    if os.environ.get("CO_NO_FASTCALL") or not os.path.exists(FASTCALL_PATH):
+        return None
+    import importlib.machinery
+    import importlib.util
+
+    loader = importlib.machinery.ExtensionFileLoader("_co_fastcall", FASTCALL_PATH)
+    spec = importlib.util.spec_from_file_location("_co_fastcall", FASTCALL_PATH, loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+
+    def table(lib, names):
+        return {n: (ctypes.cast(getattr(lib, n), ctypes.c_void_p).value,
+                    "".join(_KIND[t] for t in _SIGS[n]).encode()) for n in names}
+
+    try:
+        dev = table(load(), list(_SIGS))
+    except NativeUnavailable:
+        dev = {}
+    host = table(load_host(), HOST_SYMBOLS) if os.path.exists(HOST_LIB_PATH) else {}
+    _fast = (mod.invoke, dev, host)
+    return _fast
+
+
 def call(name, *args):
+    fast = _fast if _fast else _fastcall()
     if args and args[-1] is HOST:
         lib = load_host()
         if name not in HOST_SYMBOLS:
             raise NotImplementedError(f"{name} has no host (CPU) build; move the TensorDict "
                                       "to the HIP device")
         args = args[:-1] + (None,)
+        if fast:
+            addr, kinds = fast[2][name]
+            rc = fast[0](addr, kinds, *args)
+        else:
+            rc = getattr(lib, name)(*args)
+    elif fast and name in fast[1]:
+        addr, kinds = fast[1][name]
+        rc = fast[0](addr, kinds, *args)
     else:
-        lib = load()
-    rc = getattr(lib, name)(*args)
+        rc = getattr(load(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with status {rc}")
 

@@ -48,6 +48,9 @@ def build(force=False, verbose: bool = False) -> str:
     if not force and not _stale():
         if not os.path.exists(HOST_LIB) or os.path.getmtime(HOST_LIB) < os.path.getmtime(HOST_SRC):
             build_host(verbose=verbose)
+        if (not os.path.exists(FASTCALL_LIB)
+                or os.path.getmtime(FASTCALL_LIB) < os.path.getmtime(FASTCALL_SRC)):
+            build_fastcall(verbose=verbose)
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     obj_dir = os.path.join(OUT_DIR, "obj")
@@ -81,6 +84,7 @@ def build(force=False, verbose: bool = False) -> str:
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     build_host(verbose=verbose)
+    build_fastcall(verbose=verbose)
     return LIB
 
 
@@ -88,6 +92,26 @@ HOST_SRC = os.path.join(HERE, "host", "co_env_host.cpp")
 HOST_LIB = os.path.join(OUT_DIR, "libco_env_host.so")
 HOST_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
               "-Wall", "-Wextra"]
+
+
+FASTCALL_SRC = os.path.join(HERE, "pycall", "co_fastcall.cpp")
+FASTCALL_LIB = os.path.join(OUT_DIR, "_co_fastcall.so")
+
+
+def build_fastcall(verbose: bool = False) -> str:
+    """The CPython fast-call module (csrc/pycall): the env loop's C-ABI calls without
+    ctypes' per-call marshalling.  Optional: _native falls back to ctypes without it."""
+    import sysconfig
+
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    inc = sysconfig.get_paths()["include"]
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", inc, "-o",
+           FASTCALL_LIB + ".tmp", FASTCALL_SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(FASTCALL_LIB + ".tmp", FASTCALL_LIB)
+    return FASTCALL_LIB
 
 
 def build_host(verbose: bool = False, out: str = HOST_LIB, extra=()) -> str:
