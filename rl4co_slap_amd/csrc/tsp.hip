@@ -75,6 +75,7 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
 #ifndef CO_TSP_STEP_GROUP
 #define CO_TSP_STEP_GROUP 1
 #endif
+
 template <int G>
 __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
                                                              const int64_t* __restrict__ action,
