@@ -504,6 +504,7 @@ def main():
             out["cpu_baseline_slap"] = cpu_baseline_slap()
             out["cpu_baseline_cvrp"] = cpu_baseline_cvrp()
     if rank == 0:
+        out["build"] = _native.provenance()  # the sources the measured library came from
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -148,6 +148,29 @@ def load_host():
         return lib
 
 
+def provenance() -> dict:
+    """What the loaded device library was built from (co_build_provenance) and whether
+    that matches the sources in this tree."""
+    import json
+
+    lib = load()
+    try:
+        fn = lib.co_build_provenance
+    except AttributeError:
+        return {"source_sha256": None, "matches_tree": False}
+    fn.restype = ctypes.c_char_p
+    fn.argtypes = []
+    info = json.loads(fn().decode())
+    try:
+        from .csrc.build import source_hash
+
+        info["tree_sha256"] = source_hash()
+        info["matches_tree"] = info["tree_sha256"] == info["source_sha256"]
+    except OSError:  # sources not shipped
+        info["matches_tree"] = None
+    return info
+
+
 def exported_symbols():
     return list(_SIGS) + ["co_build_info"]
 

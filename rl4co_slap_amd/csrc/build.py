@@ -39,6 +39,43 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def source_hash() -> str:
+    """sha256 over the device library's sources, headers and the ABI header (in order)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        with open(os.path.join(HERE, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    with open(os.path.join(ROOT, "include", "co_env.h"), "rb") as fh:
+        h.update(b"co_env.h\0" + fh.read())
+    return h.hexdigest()
+
+
+def _provenance_object(obj_dir: str, verbose: bool) -> str:
+    """A host-only object exporting co_build_provenance(): the source hash the library was
+    built from, the build time and the compiler, so a run can show which sources the
+    loaded library came from (tests/test_gpu_provenance.py, bench.py "build")."""
+    import json
+    import time
+
+    ver = subprocess.run([hipcc(), "--version"], capture_output=True, text=True).stdout
+    ver = next((ln for ln in ver.splitlines() if "clang version" in ln or "HIP version" in ln), "")
+    info = json.dumps({"source_sha256": source_hash(), "built_at": time.strftime(
+        "%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "compiler": ver.strip(), "arch": ARCH})
+    src = os.path.join(obj_dir, "provenance.cpp")
+    with open(src, "w") as f:
+        f.write('extern "C" __attribute__((visibility("default"))) const char* '
+                "co_build_provenance(void) { return " + json.dumps(info) + "; }\n")
+    obj = os.path.join(obj_dir, "provenance.o")
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    cmd = [cxx, "-O2", "-fPIC", "-c", src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return obj
+
+
 def build(force=False, verbose: bool = False) -> str:
     """Compile each source to an object in parallel, then link the shared library.
     ``force="incremental"`` (``--incremental``) recompiles only objects older than their
@@ -77,6 +114,7 @@ def build(force=False, verbose: bool = False) -> str:
     jobs = min(len(SOURCES), max(1, min(os.cpu_count() or 1, 8)))
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
+    objs.append(_provenance_object(obj_dir, verbose))
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, "-x", "none"] + objs
     if verbose:
