@@ -121,11 +121,29 @@ __global__ __launch_bounds__(WAVES * 64) void slap_reward_kernel(
     const int32_t* arow = assignment + b * (int64_t)P;
     const float2* lrow = locs + b * (int64_t)L;
     constexpr int PU = 4;  // picks per lane kept in registers (S <= 256); more: a loop
+    constexpr int LU = 4;  // locations per lane (L <= 256); more: a loop
     int64_t pk[PU];
+    float2 lv[LU];
+    int32_t av = 0;
+    // every load of the instance issued before any LDS store (one memory latency):
+    // unconditional clamped addresses, the out-of-row values are never stored
 #pragma unroll
-    for (int u = 0; u < PU; ++u) pk[u] = lane + 64 * u < S ? prow[lane + 64 * u] : 0;
-    for (int c = lane; c < L; c += 64) lxy[c] = lrow[c];
-    for (int c = lane; c < P; c += 64) asg[c] = arow[c];
+    for (int u = 0; u < PU; ++u) {
+      const int sidx = lane + 64 * u;
+      pk[u] = prow[sidx < S ? sidx : S - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < LU; ++u) {
+      const int c = lane + 64 * u;
+      lv[u] = lrow[c < L ? c : L - 1];
+    }
+    av = arow[lane < P ? lane : P - 1];
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+      if (lane + 64 * u < L) lxy[lane + 64 * u] = lv[u];
+    for (int c = lane + 64 * LU; c < L; c += 64) lxy[c] = lrow[c];
+    if (lane < P) asg[lane] = av;
+    for (int c = lane + 64; c < P; c += 64) asg[c] = arow[c];
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     bool range = false;
@@ -153,23 +171,25 @@ __global__ __launch_bounds__(WAVES * 64) void slap_reward_kernel(
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    // per-order closed tour, edges summed in pick order
-    for (int o = lane; o < O; o += 64) {
-      const float2* op = pts + o * K;
+    // per-order closed tour (lane o), edges summed in pick order; the orders then added one
+    // by one in f32 (slap/env.py:136-142) from the lanes' registers (v_readlane: no LDS
+    // round trip in the serial part)
+    float total = 0.f;
+    for (int o0 = 0; o0 < O; o0 += 64) {
+      const int o = o0 + lane;
       float len = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const float2 p = op[k], q = op[(k + 1 == K) ? 0 : k + 1];
-        len += edge_len(p.x, p.y, q.x, q.y);
+      if (o < O) {
+        const float2* op = pts + o * K;
+        for (int k = 0; k < K; ++k) {
+          const float2 p = op[k], q = op[(k + 1 == K) ? 0 : k + 1];
+          len += edge_len(p.x, p.y, q.x, q.y);
+        }
       }
-      olen[o] = len;
+      const int cnt = O - o0 < 64 ? O - o0 : 64;
+      for (int j = 0; j < cnt; ++j)
+        total += -__int_as_float(__builtin_amdgcn_readlane(__float_as_int(len), j));
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {  // orders added one by one in f32 (slap/env.py:136-142)
-      float total = 0.f;
-      for (int o = 0; o < O; ++o) total += -olen[o];
-      reward[b] = total;
-    }
+    if (lane == 0) reward[b] = total;
     if (__any(range) && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
