@@ -657,9 +657,10 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
 def bench_dropin(b, n, k, world, rank, dev):
     """The path an unchanged rl4co policy takes:
     ``ConstructivePolicy(None, LogitsDecoder(stub)).forward(td, TSPEnv, greedy)`` at
-    TSP-100 B=65,536 -- per step one co_decode_step launch (greedy, logits from a fixed
-    HBM-resident [B, N] tensor: the stub decoder) and one TSPEnv._step launch, the
-    TensorDict plumbing in Python, the done poll only from step N on (env lower bound),
+    TSP-100 B=65,536 -- per step the decode and the env step (greedy, logits from a fixed
+    HBM-resident [B, N] tensor: the stub decoder) as one co_tsp_decode_step launch
+    (TSPEnv.decode_and_step), the TensorDict plumbing in Python, the done poll only from
+    step N on (env lower bound),
     then get_reward + validity and get_log_likelihood.  Also the host cost alone: the same
     loop at B = 64, where the device work is negligible."""
     from rl4co_slap_amd.envs import TSPEnv
@@ -683,7 +684,7 @@ def bench_dropin(b, n, k, world, rank, dev):
         t = max_over_ranks(wall, world, dev)
         if bb == b:
             out = {"value": world * bb * n * kk / t, "ms_per_episode": t / kk * 1e3,
-                   "batch_per_gpu": bb, "launches_per_step": 2,
+                   "batch_per_gpu": bb, "launches_per_step": 1,
                    "done_polls_per_episode": 1, "path": "ConstructivePolicy.forward + TSPEnv"}
         else:
             out["host_us_per_step_b64"] = t / kk / n * 1e6

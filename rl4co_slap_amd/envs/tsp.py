@@ -100,6 +100,53 @@ class TSPEnv(RL4COEnvBase):
                    "action_mask": mask_out, "reward": reward, "done": done})
         return td
 
+    def decode_and_step(self, td, logits, mode, temperature, tanh_clipping, action_in, seed,
+                        offset, status, key="action"):
+        """``DecodingStrategy.step`` + ``_step`` (``decoding.py:327-369``, ``tsp/env.py:67-93``)
+        in one ``co_tsp_decode_step`` launch: the same selection, log-probability, state
+        and aliasing (``current_node`` is the action tensor) as the two calls.  Returns
+        ``(action, logp)``, or None when it does not apply (CPU tensors, unknown ``i``
+        provenance for the batch-wide first-node test, non-f32 logits)."""
+        mask, i = td["action_mask"], td["i"]
+        if logits.device.type != "cuda" or mask.device != logits.device:
+            return None
+        known = self._known_i(i)
+        if known is None or logits.dtype != torch.float32 or logits.dim() != 2 \
+                or logits.stride(-1) != 1:
+            return None
+        first_in = td.get("first_node", None)
+        take = 1 if known == 0 else 0
+        if not take and first_in is None:
+            return None
+        b, n = mask.shape
+        if logits.shape != (b, n):
+            return None
+        dev = mask.device
+        mask, i = mask.contiguous(), i.contiguous()
+        first_in = first_in.contiguous() if (first_in is not None and not take) else None
+        ain = action_in.long().contiguous() if action_in is not None else None
+        act = torch.empty(b, dtype=torch.int64, device=dev)
+        logp = torch.empty(b, dtype=torch.float32, device=dev)
+        mask_out = torch.empty_like(mask)
+        i_out = torch.empty_like(i)
+        first_out = torch.empty(b, dtype=torch.int64, device=dev)
+        done = torch.empty(b, dtype=torch.bool, device=dev)
+        reward = torch.empty(b, dtype=torch.bool, device=dev)
+        nat.call("co_tsp_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
+                 float(tanh_clipping), float(temperature), mode, nat.ptr(ain), nat.ptr(act),
+                 nat.ptr(logp), seed, offset, nat.ptr(mask_out), nat.ptr(i), nat.ptr(i_out),
+                 nat.ptr(first_in), nat.ptr(first_out), take, nat.ptr(done), nat.ptr(reward),
+                 None, nat.ptr(status), nat.stream_of(mask))
+        sel = action_in if action_in is not None else act
+        self._remember_i(i_out, known + 1)
+        lb = self._known_lb(td["action_mask"])
+        if lb is not None:
+            self._remember_lb(mask_out, lb - 1)
+        td.set(key, sel)
+        td.update({"first_node": first_out, "current_node": sel, "i": i_out,
+                   "action_mask": mask_out, "reward": reward, "done": done})
+        return sel, logp
+
     def _get_reward(self, td, actions, check: bool = False) -> torch.Tensor:
         """``tsp/env.py:157-173``: -tour length, fused with the permutation check.  A
         multistart td's un-replicated ``locs`` (``RepeatedRows``) is read in place: env

@@ -114,9 +114,14 @@ class ConstructivePolicy(nn.Module):
         step = 0
         while step < lb or not td["done"].all():
             logits, mask = self.decoder(td, hidden, num_starts)
-            td = strategy.step(logits, mask, td,
-                               action=actions[..., step] if actions is not None else None)
-            td = env.step(td)["next"]
+            act = actions[..., step] if actions is not None else None
+            # decode + env step as one launch where the env provides it (TSP), else both
+            nxt = strategy.step_env_fused(logits, mask, td, env, action=act)
+            if nxt is None:
+                td = strategy.step(logits, mask, td, action=act)
+                td = env.step(td)["next"]
+            else:
+                td = nxt
             step += 1
             if step > max_steps:
                 log.error(f"Exceeded maximum number of steps ({max_steps}) duing decoding")

@@ -21,6 +21,7 @@ from ..td import TensorDict
 from .ops import batchify, gather_by_index, unbatchify, unbatchify_and_gather
 
 _MODES = {"greedy": 0, "sampling": 1, "evaluate": 2}
+_NO_FUSED = bool(__import__("os").environ.get("CO_NO_FUSED_STEP"))  # A/B switch (tests, diag)
 
 
 def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, action=None,
@@ -184,9 +185,11 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
             self._status = nat.scratch_status(logits.device)
         mode = self._mode()
         act_in = action if mode == "evaluate" else None
+        seed = getattr(self, "_seed_carry", None)
+        self._seed_carry = None
         sel, logp, full = decode_step(logits, mask, mode, self.temperature, self.tanh_clipping,
                                       action=act_in, return_full=self.store_all_logp,
-                                      offset=self._step_idx, status=self._status,
+                                      seed=seed, offset=self._step_idx, status=self._status,
                                       top_k=self.top_k, top_p=self.top_p)
         self._step_idx += 1
         if mode == "evaluate":
@@ -197,6 +200,36 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         td.set(self.key, sel)
         self.actions.append(sel)
         self.logprobs.append(out_lp)
+        return td
+
+    def step_env_fused(self, logits, mask, td, env, action=None):
+        """``self.step`` followed by ``env.step`` as ONE launch, when the env offers it
+        (``TSPEnv.decode_and_step``: ``co_tsp_decode_step``) and nothing in between could
+        observe the difference: the env's own ``step``, the mask the env holds, no full
+        log-probabilities / top-k / top-p.  Same outputs, same RNG use; returns the next
+        td, or None when the fused path does not apply (the caller runs both steps)."""
+        fused = getattr(env, "decode_and_step", None)
+        if (fused is None or _NO_FUSED or self.store_all_logp or self.improvement_method_mode
+                or self.top_k > 0 or 0.0 < self.top_p < 1.0 or not self.mask_logits
+                or getattr(env, "_torchrl_mode", False) or mask is not td.get("action_mask")):
+            return None
+        mode = self._mode()
+        if mode not in _MODES:
+            return None
+        if self._status is None:
+            self._status = nat.scratch_status(logits.device)
+        seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
+        out = fused(td, logits, _MODES[mode], self.temperature, self.tanh_clipping,
+                    action if mode == "evaluate" else None, seed, self._step_idx, self._status,
+                    self.key)
+        if out is None:
+            if mode == "sampling":  # the seed draw above stands in for decode_step's
+                self._seed_carry = seed
+            return None
+        self._step_idx += 1
+        sel, logp = out
+        self.actions.append(sel)
+        self.logprobs.append(logp)
         return td
 
     @abc.abstractmethod
