@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP32_VECTOR_PEAK_TFS = 157.3  # MI355X FP32 vector (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -583,7 +584,17 @@ def annotate_modes(modes, n, world):
             byts = f(m)
             gbs = m["value"] / world * byts / 1e9
             m.update({"alg_bytes_per_env_step": byts, "achieved_GBps_per_gpu": gbs,
-                      "hbm_frac": gbs / HBM_PEAK_GBS})
+                      "hbm_frac": gbs / HBM_PEAK_GBS, "bound": "hbm"})
+    # the in-kernel nearest policies are O(N^2) vector ALU work on register-resident
+    # coordinates, not HBM traffic: per env-step one squared distance
+    # per candidate (2 sub + 2 mul + 1 add = 5 FLOP), against the 157.3 TFLOP/s FP32
+    # vector peak (MI355X_MICROARCH.md)
+    for name, cand in (("tsp_fused_nearest", n), ("cvrp_fused_nearest", n + 1)):
+        if name in modes and "value" in modes[name]:
+            m = modes[name]
+            tf = m["value"] / world * cand * 5 / 1e12
+            m.update({"bound": "valu (O(N^2) distance scans, serial step chain)",
+                      "achieved_TFLOPs_per_gpu": tf, "valu_frac": tf / FP32_VECTOR_PEAK_TFS})
 
 
 def bench_slap(b, k, world, rank, dev, stepwise=True):
