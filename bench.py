@@ -575,7 +575,11 @@ def annotate_modes(modes, n, world):
         "pomo_tsp100_certified": lambda m: 6 * n + 54,
         "cvrp_fused_nearest": lambda m: (8 + 12 * n + 8 * m["episode_steps"] + 10 * (n + 1) + 25)
         / m["episode_steps"],
-        "cvrp_stepwise_graph": lambda m: 7 * n + 33 + (16 * m["episode_steps"] + 12)
+        # fused policy: locs 8(N+1) + mask, visited N+1 each + demand 4N + 16 B state read;
+        # visited, mask N+1 each + 22 B state written -- plus the episode's reward kernel
+        "cvrp_stepwise_graph": lambda m: 16 * n + 50 + (16 * m["episode_steps"] + 12)
+        / m["episode_steps"],
+        "cvrp_stepwise_graph_pair": lambda m: 7 * n + 33 + (16 * m["episode_steps"] + 12)
         / m["episode_steps"],
     }
     for name, f in per_step.items():
@@ -741,14 +745,19 @@ def bench_cvrp(b, n, k, world, rank, dev):
                                  "input_batches_cycled": n_rot,
                                  "launch_us": ev / kk * 1e6}
     del fus
-    sw = CVRPStepwiseEpisode(td).capture()
-    wall, ev = timed(sw.replay, k, 1, world, dev)
-    t = max_over_ranks(wall, world, dev)
-    assert sw.T == T and int(sw.status.item()) == 0, "CVRP stepwise episode status"
     steps_one = sum_over_ranks(b * T, world, dev)
-    out["cvrp_stepwise_graph"] = {"value": steps_one * k / t, "ms_per_episode": t / k * 1e3,
-                                  "batch_per_gpu": b, "episode_steps": T,
-                                  "bytes_per_env_step": 7 * n + 33}
+    # nearest policy fused with each step (co_cvrp_nearest_step, one launch per step), then
+    # the co_cvrp_nearest_action + co_cvrp_step pair (the env step as any policy drives it)
+    for name, fused, byts in (("cvrp_stepwise_graph", True, 16 * n + 50),
+                              ("cvrp_stepwise_graph_pair", False, 7 * n + 33)):
+        sw = CVRPStepwiseEpisode(td, fused_policy=fused).capture()
+        wall, ev = timed(sw.replay, k, 1, world, dev)
+        t = max_over_ranks(wall, world, dev)
+        assert sw.T == T and int(sw.status.item()) == 0, "CVRP stepwise episode status"
+        out[name] = {"value": steps_one * k / t, "ms_per_episode": t / k * 1e3,
+                     "batch_per_gpu": b, "episode_steps": T, "bytes_per_env_step": byts,
+                     "launches_per_step": 1 if fused else 2}
+        del sw
     return out
 
 

@@ -234,6 +234,17 @@ int co_cvrp_nearest_action(int64_t batch, int64_t num_loc, const float* locs,
                            int64_t* action_out, void* stream);
 int co_slap_closest_free_action(int64_t batch, int64_t num_slots, const float* depot_loc_dist,
                                 const uint8_t* action_mask, int64_t* action_out, void* stream);
+/* The nearest-feasible bench policy fused with CVRPEnv._step + get_action_mask
+ * (cvrp/env.py:73-149): the action co_cvrp_nearest_action would pick from (mask_in,
+ * cur_in) is written to action_out and applied as co_cvrp_step does, in one launch.
+ * In place (visited_out == visited_in, mask_out == mask_in) is allowed.  Results are
+ * identical to the two calls (which it falls back to for N + 1 > 128). */
+int co_cvrp_nearest_step(int64_t batch, int64_t num_loc, const float* locs, const float* demand,
+                         const float* used_in, float* used_out, const float* vehicle_capacity,
+                         const uint8_t* visited_in, uint8_t* visited_out,
+                         const uint8_t* mask_in, const int64_t* current_in, int64_t* action_out,
+                         int64_t* current_out, uint8_t* done, uint8_t* reward, uint8_t* mask_out,
+                         int32_t* status, int32_t* not_done, void* stream);
 /* The closest-free bench policy fused with SLAPEnv._step (slap/env.py:38-93): the
  * action co_slap_closest_free_action would pick is written to action_out and applied
  * as co_slap_step does (assign_out = assign_in with [b, p] = action; in-place allowed),

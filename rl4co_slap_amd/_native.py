@@ -45,6 +45,8 @@ _SIGS = {
     "co_distance_matrix": [_i64, _i64, _p, _p, _p],
     "co_tsp_nearest_action": [_i64, _i64, _p, _p, _p, _i32, _p, _p],
     "co_cvrp_nearest_action": [_i64, _i64, _p, _p, _p, _p, _p],
+    "co_cvrp_nearest_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                             _p, _p, _p],
     "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],
     "co_slap_closest_step": [_i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                              _p, _p],

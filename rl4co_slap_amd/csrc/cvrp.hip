@@ -381,6 +381,153 @@ __global__ __launch_bounds__(256) void cvrp_nearest_group_kernel(int64_t B, int 
   }
 }
 
+// The nearest-feasible bench policy fused with the step (co_cvrp_nearest_step: the
+// results of co_cvrp_nearest_action + co_cvrp_step in one launch).  A 256-thread
+// workgroup owns a tile of 16 rows, G = 16 lanes per row; lane sl owns nodes
+// c = sl + k*16 (k < KM).  The tile's visited and mask bytes (16 x (N+1), a multiple of 16
+// bytes, so the tile starts 16-B aligned) move between HBM and LDS as 16-B chunks; the
+// lanes' coordinates and demands are loaded straight into registers (coalesced across
+// the group), all before the first use.  The current node's coordinates and the chosen
+// node's demand come from their owner lanes by shuffle; the policy is the group argmin of
+// the torch-exact Euclidean distance over feasible customers (lowest index on ties, depot
+// when none); the step then updates visited / capacity and recomputes the mask in
+// registers (cvrp/env.py:73-105,137-149).  One not-done atomic per workgroup.
+constexpr int kCnsRows = 16;
+template <int KM>
+__global__ __launch_bounds__(256) void cvrp_nearest_step_kernel(
+    int64_t B, int N, const float2* __restrict__ locs, const float* __restrict__ demand,
+    const float* __restrict__ used_in, float* __restrict__ used_out,
+    const float* __restrict__ vcap, const uint8_t* vis_in, uint8_t* vis_out,
+    const uint8_t* mask_in, const int64_t* __restrict__ cur_in, int64_t* __restrict__ action_out,
+    int64_t* __restrict__ cur_out, uint8_t* __restrict__ done, uint8_t* __restrict__ reward,
+    uint8_t* mask_out, bool vec, int32_t* not_done) {
+  constexpr int G = 16;
+  __shared__ __attribute__((aligned(16))) uint8_t s_vis[kCnsRows * 16 * KM];
+  __shared__ __attribute__((aligned(16))) uint8_t s_mk[kCnsRows * 16 * KM];
+  __shared__ int s_left[4];
+  const int tid = threadIdx.x, lane = tid & 63, sl = tid % G, row = tid / G;
+  const int NC = N + 1;
+  for (int64_t tile = blockIdx.x; tile * kCnsRows < B; tile += gridDim.x) {
+    const int64_t row0 = tile * kCnsRows;
+    const int rows = (int)((B - row0) < kCnsRows ? (B - row0) : kCnsRows);
+    const int nbytes = rows * NC, nchunks = (nbytes + 15) >> 4;
+    const bool valid = row < rows;
+    const int64_t r = row0 + (valid ? row : 0);
+    // every global load before the barrier: the byte tiles (16-B chunks), the lane's
+    // coordinates and demands at clamped columns, the row scalars
+    uint4 cv = make_uint4(0, 0, 0, 0), cm = cv;
+    if (tid < nchunks) {
+      cv = tile_load(vis_in + row0 * NC, tid << 4, nbytes, vec);
+      cm = tile_load(mask_in + row0 * NC, tid << 4, nbytes, vec);
+    }
+    const float2* lrow = locs + r * NC;
+    const float* drow = demand + r * (int64_t)N;
+    float2 q[KM];
+    float dm[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int c = sl + k * G;
+      const int cc = c <= N ? c : N;
+      q[k] = lrow[cc];
+      dm[k] = drow[cc >= 1 ? cc - 1 : 0];
+    }
+    int64_t c0 = cur_in[r];
+    const float u_in = used_in[r], cap = vcap[r];
+    if (tid < nchunks) {
+      *reinterpret_cast<uint4*>(s_vis + (tid << 4)) = cv;
+      *reinterpret_cast<uint4*>(s_mk + (tid << 4)) = cm;
+    }
+    __syncthreads();
+    uint8_t mk[KM], vs[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int c = sl + k * G;
+      const int o = row * NC + (c <= N ? c : N);
+      mk[k] = s_mk[o];
+      vs[k] = s_vis[o];
+    }
+    c0 = (c0 < 0 || c0 > N) ? 0 : c0;
+    float2 pc = q[0];
+#pragma unroll
+    for (int k = 1; k < KM; ++k) pc = (k == (int)(c0 / G)) ? q[k] : pc;
+    const int g0 = lane - sl;
+    const float px = __shfl(pc.x, g0 + (int)(c0 % G), 64);
+    const float py = __shfl(pc.y, g0 + (int)(c0 % G), 64);
+    // the policy (co_cvrp_nearest_action)
+    float best = __builtin_inff();
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int c = sl + k * G;
+      const float d = edge_len(px, py, q[k].x, q[k].y);
+      const bool take = (c >= 1) & (c <= N) & (mk[k] != 0) & (d < best);
+      best = take ? d : best;
+      bi = take ? c : bi;
+    }
+    grp_argmin_split<G>(best, bi);
+    const int a = bi == 0x7fffffff ? 0 : bi;
+    // the step (cvrp/env.py:79-85): d = demand[clamp(a - 1, 0, N - 1)], from its owner lane
+    const int nd = a >= 1 ? a : 1;
+    float dsel = dm[0];
+#pragma unroll
+    for (int k = 1; k < KM; ++k) dsel = (k == nd / G) ? dm[k] : dsel;
+    dsel = __shfl(dsel, g0 + nd % G, 64);
+    const float u = (u_in + dsel) * ((a != 0) ? 1.0f : 0.0f);
+    int vsum = 0, anyf = 0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int c = sl + k * G;
+      if (c <= N) {
+        const uint8_t v = (uint8_t)(vs[k] | (c == a));
+        vs[k] = v;
+        vsum += v;
+        if (c >= 1) {  // cvrp/env.py:140-144: visited | demand + used > capacity (strict)
+          const bool masked = (v != 0) || (dm[k] + u > cap);
+          mk[k] = !masked;
+          anyf |= !masked;
+        }
+      }
+    }
+    vsum = (int)grp_reduce<G>((uint32_t)vsum, [](uint32_t x, uint32_t y) { return x + y; });
+    anyf = grp_max_int<G>(anyf);
+    if (sl == 0) mk[0] = !((a == 0) && anyf);  // node 0 is lane 0's k = 0
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int c = sl + k * G;
+        if (c <= N) {
+          s_vis[row * NC + c] = vs[k];
+          s_mk[row * NC + c] = mk[k];
+        }
+      }
+    }
+    const bool dn = vsum == N + 1;
+    if (not_done) {
+      const int left = __popcll(__ballot(valid && sl == 0 && !dn));
+      if (lane == 0) s_left[tid >> 6] = left;
+    }
+    __syncthreads();
+    if (tid < nchunks) {
+      tile_store(vis_out + row0 * NC, tid << 4, nbytes, vec,
+                 *reinterpret_cast<const uint4*>(s_vis + (tid << 4)));
+      tile_store(mask_out + row0 * NC, tid << 4, nbytes, vec,
+                 *reinterpret_cast<const uint4*>(s_mk + (tid << 4)));
+    }
+    if (valid && sl == 0) {
+      action_out[r] = a;
+      used_out[r] = u;
+      cur_out[r] = a;
+      done[r] = dn;
+      reward[r] = 0;
+    }
+    if (not_done && tid == 0) {
+      const int left = s_left[0] + s_left[1] + s_left[2] + s_left[3];
+      if (left) atomicAdd(not_done, left);
+    }
+    __syncthreads();  // the LDS tiles are reused by the next tile
+  }
+}
+
 __global__ __launch_bounds__(256) void cvrp_mask_kernel(int64_t B, int N, const float* demand,
                                                         const float* used, const float* vcap,
                                                         const uint8_t* visited,
@@ -919,5 +1066,45 @@ extern "C" int co_cvrp_nearest_action(int64_t B, int64_t N, const float* locs,
   else if (N <= 320) CO_CNG(32, 10);
   else CO_CNG(64, 0);
 #undef CO_CNG
+  return launch_status();
+}
+
+extern "C" int co_cvrp_nearest_step(int64_t B, int64_t N, const float* locs, const float* demand,
+                                    const float* used_in, float* used_out, const float* vcap,
+                                    const uint8_t* vis_in, uint8_t* vis_out,
+                                    const uint8_t* mask_in, const int64_t* cur_in,
+                                    int64_t* action_out, int64_t* cur_out, uint8_t* done,
+                                    uint8_t* reward, uint8_t* mask_out, int32_t* status,
+                                    int32_t* not_done, void* stream) {
+  if (B < 0 || N <= 0) return CO_E_INVAL;
+  if (B == 0) return CO_OK;
+  if (!locs || !demand || !used_in || !used_out || !vcap || !vis_in || !vis_out || !mask_in ||
+      !cur_in || !action_out || !cur_out || !done || !reward || !mask_out)
+    return CO_E_INVAL;
+  if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  if (N + 1 > 16 * 8) {  // the two launches it fuses
+    int rc = co_cvrp_nearest_action(B, N, locs, mask_in, cur_in, action_out, stream);
+    if (rc != CO_OK) return rc;
+    return co_cvrp_step(B, N, action_out, demand, used_in, used_out, vcap, vis_in, vis_out,
+                        cur_out, done, reward, mask_out, status, not_done, stream);
+  }
+  // 16-B chunk access when every byte tile starts 16-B aligned (16 x (N+1) bytes per tile)
+  const bool vec = ((reinterpret_cast<uintptr_t>(vis_in) | reinterpret_cast<uintptr_t>(vis_out) |
+                     reinterpret_cast<uintptr_t>(mask_in) |
+                     reinterpret_cast<uintptr_t>(mask_out)) & 15) == 0;
+  const int64_t tiles = (B + kCnsRows - 1) / kCnsRows;
+  const dim3 grid((unsigned)(tiles < 65536 ? tiles : 65536));
+  const float2* l2 = reinterpret_cast<const float2*>(locs);
+  hipStream_t s = (hipStream_t)stream;
+#define CO_CNS(KM)                                                                            \
+  hipLaunchKernelGGL((cvrp_nearest_step_kernel<KM>), grid, dim3(256), 0, s, B, (int)N, l2,     \
+                     demand, used_in, used_out, vcap, vis_in, vis_out, mask_in, cur_in,        \
+                     action_out, cur_out, done, reward, mask_out, vec, not_done)
+  const int km = (int)((N + 1 + 15) / 16);
+  if (km <= 2) CO_CNS(2);
+  else if (km <= 4) CO_CNS(4);
+  else if (km <= 7) CO_CNS(7);
+  else CO_CNS(8);
+#undef CO_CNS
   return launch_status();
 }

@@ -328,8 +328,12 @@ class CVRPStepwiseEpisode:
     only repeat the depot action)."""
 
     def __init__(self, td, vehicle_capacity: float = 1.0, max_steps: int = None,
-                 chunk: int = 8):
+                 chunk: int = 8, fused_policy: bool = True):
         locs = td["locs"]
+        # fused_policy: co_cvrp_nearest_step (policy + step, one launch); False: the
+        # co_cvrp_nearest_action + co_cvrp_step pair (the env step alone, as a policy-agnostic
+        # loop calls it)
+        self.fused_policy = fused_policy
         d = locs.device
         self.device = d
         b, n = locs.shape[0], locs.shape[1]
@@ -364,13 +368,22 @@ class CVRPStepwiseEpisode:
 
     def _step(self, t, s):
         k, k1 = t % 2, (t + 1) % 2
+        nd = nat.ptr(self.not_done[t:]) if t >= self.n else None
+        if self.fused_policy:  # the bench policy fused with the step: one launch
+            nat.call("co_cvrp_nearest_step", self.b, self.n, nat.ptr(self.locs),
+                     nat.ptr(self.demand), nat.ptr(self.used[t]), nat.ptr(self.used[t + 1]),
+                     nat.ptr(self.vcap_t), nat.ptr(self.visited[k]), nat.ptr(self.visited[k1]),
+                     nat.ptr(self.mask[k]), nat.ptr(self.cur[t]), nat.ptr(self.acts[t]),
+                     nat.ptr(self.cur[t + 1]), nat.ptr(self.done), nat.ptr(self.step_reward),
+                     nat.ptr(self.mask[k1]), nat.ptr(self.status), nd, s)
+            return
         nat.call("co_cvrp_nearest_action", self.b, self.n, nat.ptr(self.locs),
                  nat.ptr(self.mask[k]), nat.ptr(self.cur[t]), nat.ptr(self.acts[t]), s)
         nat.call("co_cvrp_step", self.b, self.n, nat.ptr(self.acts[t]), nat.ptr(self.demand),
                  nat.ptr(self.used[t]), nat.ptr(self.used[t + 1]), nat.ptr(self.vcap_t),
                  nat.ptr(self.visited[k]), nat.ptr(self.visited[k1]), nat.ptr(self.cur[t + 1]),
                  nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.mask[k1]),
-                 nat.ptr(self.status), nat.ptr(self.not_done[t:]) if t >= self.n else None, s)
+                 nat.ptr(self.status), nd, s)
 
     def _ranges(self):
         first = min(self.n, self.max_steps)

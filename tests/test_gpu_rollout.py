@@ -217,8 +217,8 @@ def _check_cvrp(state, a, r, tdf):
     assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
 
 
-@pytest.mark.parametrize("b,n", [(1, 5), (64, 20), (256, 100), (33, 63), (17, 130)])
-@pytest.mark.parametrize("kind", ["fused", "stepwise"])
+@pytest.mark.parametrize("b,n", [(1, 5), (64, 20), (256, 100), (33, 63), (9, 127), (17, 130)])
+@pytest.mark.parametrize("kind", ["fused", "stepwise", "stepwise_pair"])
 def test_cvrp_rollout_matches_oracle(dev, b, n, kind):
     from rl4co_slap_amd.rollout.engine import CVRPFusedEpisode, CVRPStepwiseEpisode
 
@@ -235,7 +235,10 @@ def test_cvrp_rollout_matches_oracle(dev, b, n, kind):
         torch.cuda.synchronize()
         _check_cvrp(ep.final_state(), a, r, tdf)
     else:
-        ep = CVRPStepwiseEpisode(td, vehicle_capacity=vcap, chunk=4).capture()
+        # stepwise: co_cvrp_nearest_step (policy + step in one launch); stepwise_pair: the
+        # co_cvrp_nearest_action + co_cvrp_step pair
+        ep = CVRPStepwiseEpisode(td, vehicle_capacity=vcap, chunk=4,
+                                 fused_policy=kind == "stepwise").capture()
         for _ in range(2):  # replays are repeatable
             T = ep.replay()
             torch.cuda.synchronize()

@@ -96,3 +96,43 @@ def test_td_standin_batchify_roundtrip():
     assert torch.equal(tb["locs"][2 * 3 + 1], td["locs"][1])
     tu = unbatchify(tb, 4)
     assert tu.batch_size == (3, 4) and torch.equal(tu["locs"][:, 3], td["locs"])
+
+
+def test_fastcall_path_matches_ctypes_on_the_host_build():
+    """The METH_FASTCALL trampoline (csrc/pycall/co_fastcall.cpp) is built, carries a kinds
+    string for every bound entry point, and gives the ctypes path's results (a host CVRP
+    reset: int64, pointer and float arguments, None as the null stream)."""
+    fast = _native._fastcall()
+    assert fast is not None, "_co_fastcall.so missing: run the build"
+    invoke, dev, host = fast
+    assert set(dev) == set(_native._SIGS)  # every int-returning entry point
+    assert set(host) == set(_native.HOST_SYMBOLS)
+    assert all(len(k) == len(_native._SIGS[n]) for n, (_, k) in dev.items())
+    lib = _native.load_host()
+    b, n = 5, 7
+    gen = torch.Generator().manual_seed(0)
+    depot = torch.rand(b, 2, generator=gen)
+    locs = torch.rand(b, n, 2, generator=gen)
+    dem = torch.rand(b, n, generator=gen) * 0.3
+    outs = []
+    for path in ("fast", "ctypes"):
+        o = {"locs": torch.empty(b, n + 1, 2), "cur": torch.empty(b, dtype=torch.int64),
+             "used": torch.empty(b), "vcap": torch.empty(b), "vis": torch.empty(b, n + 1,
+                                                                                 dtype=torch.uint8),
+             "mask": torch.empty(b, n + 1, dtype=torch.bool)}
+        args = (b, n, depot.data_ptr(), locs.data_ptr(), dem.data_ptr(), 0.75,
+                o["locs"].data_ptr(), o["cur"].data_ptr(), o["used"].data_ptr(),
+                o["vcap"].data_ptr(), o["vis"].data_ptr(), o["mask"].data_ptr(), None)
+        if path == "fast":
+            addr, kinds = host["co_cvrp_reset"]
+            assert invoke(addr, kinds, *args) == 0
+        else:
+            assert lib.co_cvrp_reset(*args) == 0
+        outs.append(o)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    assert (outs[0]["vcap"] == 0.75).all()
+    # an error status comes back through both paths alike
+    addr, kinds = host["co_cvrp_reset"]
+    bad = (-1, n) + (0,) * 3 + (1.0,) + (0,) * 7
+    assert invoke(addr, kinds, *bad) == lib.co_cvrp_reset(*bad) != 0
