@@ -691,9 +691,12 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
 // so each action load of a wave is one coalesced 512-B piece of a row that no other
 // workgroup touches.  The tile's [64, N+1] coordinates (and, with `check`, its [64, N]
 // demand rows) are staged once into LDS by LDS-DMA.
-// * Walker waves split the steps into contiguous ranges (a range's first edge starts
-//   from the action before it), double-buffer U-step batches of action rows and sum the
-//   edges (f32 per batch, f64 across batches); they also flag out-of-range indices.
+// * Walker waves take U-step batches of action rows round-robin (walker p: batches p,
+//   p + P, ...; a batch's first edge starts from the action before it, loaded with the
+//   batch), double-buffered, and sum the edges (f32 per batch, f64 across batches); they
+//   also flag out-of-range indices.  Round-robin keeps the walkers together on a short
+//   window of steps that the scanner follows, so its re-reads of the same action lines
+//   are L2 hits (contiguous per-walker ranges left most lines to be fetched twice).
 // * With `check`, wave 0 is the scanner: it walks the whole episode in step order with
 //   a two-stage pipeline (batch k+1's action rows in flight -- L2 hits after the walkers
 //   -- while batch k is processed): marks the node in the instance's LDS visited words
@@ -702,7 +705,7 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
 //   runs the reference's sequential f32 capacity scan (cvrp/env.py:180-190) in its exact
 //   operation order.  Its serial chain overlaps the walkers instead of following them.
 #ifndef CO_CVRPR_U
-#define CO_CVRPR_U 8
+#define CO_CVRPR_U 4
 #endif
 #ifndef CO_CVRPR_Q
 #define CO_CVRPR_Q 8
@@ -765,20 +768,19 @@ __global__ __launch_bounds__(64 * Q) void cvrp_reward_tile_kernel(
   };
   const int P = check ? Q - 1 : Q;  // walker waves
   const int p = check ? q - 1 : q;
-  const int R = (T + P - 1) / P;
-  const int m_lo = p * R < T ? p * R : T;
-  const int m_hi = m_lo + R < T ? m_lo + R : T;
-  int64_t bufA[U], bufB[U], a_prev = 0;
-  auto wload = [&](int64_t (&dst)[U], int t0) {  // walker rows, clamped into [m_lo, m_hi)
+  const int nbt = (T + U - 1) / U;  // U-step batches, walker p takes p, p + P, ...
+  int64_t bufA[U], bufB[U], prevA = 0, prevB = 0;
+  auto wload = [&](int64_t (&dst)[U], int64_t& prev, int j) {  // batch j (+ the step before)
+    const int t0 = j * U;
+    prev = t0 > 0 ? ap[(int64_t)(t0 - 1) * st] : 0;  // step 0 starts from the depot
 #pragma unroll
-    for (int u = 0; u < U; ++u) dst[u] = ap[(int64_t)(t0 + u < m_hi ? t0 + u : m_hi - 1) * st];
+    for (int u = 0; u < U; ++u) dst[u] = ap[(int64_t)(t0 + u < T ? t0 + u : T - 1) * st];
   };
   if (scanner) {
     sload(a0, 0);
     sload(a1, SU);
-  } else if (m_lo < m_hi) {
-    if (m_lo > 0) a_prev = ap[(int64_t)(m_lo - 1) * st];
-    wload(bufA, m_lo);
+  } else if (p < nbt) {
+    wload(bufA, prevA, p);
   }
   if (check)
     for (int k = threadIdx.x; k < 64 * L.VW; k += 64 * Q) s_vis[k] = 0u;
@@ -849,53 +851,50 @@ __global__ __launch_bounds__(64 * Q) void cvrp_reward_tile_kernel(
     if (lane == 0) s_tm[2] = __builtin_readcyclecounter() - tm0;
 #endif
   } else {
-    // ---- walkers: edges (+ visited words) over a contiguous step range
+    // ---- walkers: edges (+ visited words) over round-robin U-step batches
     bool range = false;
     int nonzero = 0;
     uint32_t* vw = s_vis + lane * L.VW;
-    if (m_lo < m_hi) {
-      // the point before the range: the depot at m = 0, else the previous step's node
-      bool pok = a_prev >= 0 && a_prev <= N;
-      float2 pt = xy[pok ? (int)a_prev : 0];
-      auto run = [&](const int64_t (&src)[U], int t0) {
-        const int cnt = m_hi - t0 < U ? m_hi - t0 : U;  // wave-uniform
-        float acc = 0.f;
+    auto run = [&](const int64_t (&src)[U], int64_t prev, int j) {
+      const int t0 = j * U;
+      const int cnt = T - t0 < U ? T - t0 : U;  // wave-uniform
+      bool pok = prev >= 0 && prev <= N;  // the point before the batch
+      float2 pt = xy[pok ? (int)prev : 0];
+      float acc = 0.f;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u < cnt) {
-            const bool ok = src[u] >= 0 && src[u] <= N;
-            const int a = ok ? (int)src[u] : 0;
-            const float2 qq = xy[a];
-            if (check) {  // no-return ds_or; node 0 (depot / out of range) is not counted
-              __hip_atomic_fetch_or(&vw[a >> 5], 1u << (a & 31), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-              nonzero += a != 0;
-            }
-            if (pok && ok) {
-              const float dx = qq.x - pt.x, dy = qq.y - pt.y;
-              acc += sqrtf(dx * dx + dy * dy);
-            }
-            range |= !ok;
-            pt = qq;
-            pok = ok;
+      for (int u = 0; u < U; ++u) {
+        if (u < cnt) {
+          const bool ok = src[u] >= 0 && src[u] <= N;
+          const int a = ok ? (int)src[u] : 0;
+          const float2 qq = xy[a];
+          if (check) {  // no-return ds_or; node 0 (depot / out of range) is not counted
+            __hip_atomic_fetch_or(&vw[a >> 5], 1u << (a & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            nonzero += a != 0;
           }
+          if (pok && ok) {
+            const float dx = qq.x - pt.x, dy = qq.y - pt.y;
+            acc += sqrtf(dx * dx + dy * dy);
+          }
+          range |= !ok;
+          pt = qq;
+          pok = ok;
         }
-        len += (double)acc;
-      };
-      const int nb = (m_hi - m_lo + U - 1) / U;
-      int k = 0;
-      for (; k + 1 < nb; k += 2) {
-        wload(bufB, m_lo + (k + 1) * U);
-        run(bufA, m_lo + k * U);
-        if (k + 2 < nb) wload(bufA, m_lo + (k + 2) * U);
-        run(bufB, m_lo + (k + 1) * U);
       }
-      if (k < nb) run(bufA, m_lo + k * U);
-      if (m_hi == T) {  // owner of the last step: the closing edge starts here
+      len += (double)acc;
+      if (t0 + cnt == T) {  // owner of the last step: the closing edge starts here
         s_last[lane] = pt;
         s_lok[lane] = pok;
       }
+    };
+    int j = p;
+    for (; j + P < nbt; j += 2 * P) {
+      wload(bufB, prevB, j + P);
+      run(bufA, prevA, j);
+      if (j + 2 * P < nbt) wload(bufA, prevA, j + 2 * P);
+      run(bufB, prevB, j + P);
     }
+    if (j < nbt) run(bufA, prevA, j);
     if (range) s_range[lane] = 1;
     if (check && nonzero) atomicAdd(&s_cnt[lane], nonzero);
 #ifdef CO_CVRPR_TIMING
