@@ -27,6 +27,7 @@ import torch
 from .. import _native as nat
 from ..td import TensorDict
 from ..utils.ops import get_num_starts, select_start_nodes
+from ..utils.pool import OutputPool
 
 
 def _default_device():
@@ -73,6 +74,8 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         # lower bounds on the steps before `done` can be all true, keyed by the state
         # tensor the bound is about (same weakref/version bookkeeping)
         self._lb_known = {}
+        # the step functions' fresh outputs (utils/pool.py); CO_NO_POOL=1: torch.empty
+        self._pool = None if os.environ.get("CO_NO_POOL") else OutputPool()
 
     # -- seeding (base.py:288-291) ---------------------------------------------
     def set_seed(self, seed: Optional[int]):
@@ -204,6 +207,18 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         if rec is None or rec[0]() is not t or rec[1] != t._version:
             return None
         return rec[2]
+
+    # -- step outputs -------------------------------------------------------------
+    def _out(self, shape, dtype, device, stream):
+        """A fresh output tensor for a step function: from the env's pool when nothing
+        else refers to a pooled one (indistinguishable from a new allocation), else
+        torch.empty.  Host-side knowledge about a reused tensor's old contents is dropped."""
+        if self._pool is None:
+            return torch.empty(shape, dtype=dtype, device=device)
+        t = self._pool.empty(shape, dtype, device, stream)
+        self._i_known.pop(id(t), None)
+        self._lb_known.pop(id(t), None)
+        return t
 
     # -- done-poll lower bounds ---------------------------------------------------
     def _remember_lb(self, t: torch.Tensor, steps: int):

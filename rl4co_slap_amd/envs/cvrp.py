@@ -122,16 +122,16 @@ class CVRPEnv(RL4COEnvBase):
                                                (action, demand, used, vcap, visited))
         b, n = demand.shape
         dev = demand.device
-        used_out = torch.empty_like(used)
-        visited_out = torch.empty_like(visited)
-        cur = torch.empty((b, 1), dtype=torch.int64, device=dev)
-        done = torch.empty(b, dtype=torch.bool, device=dev)
-        reward = torch.empty(b, dtype=torch.bool, device=dev)
-        mask = torch.empty((b, n + 1), dtype=torch.bool, device=dev)
+        s = nat.stream_of(demand)
+        used_out = self._out(used.shape, used.dtype, dev, s)
+        visited_out = self._out(visited.shape, visited.dtype, dev, s)
+        cur = self._out((b, 1), torch.int64, dev, s)
+        done = self._out((b,), torch.bool, dev, s)
+        reward = self._out((b,), torch.bool, dev, s)
+        mask = self._out((b, n + 1), torch.bool, dev, s)
         nat.call("co_cvrp_step", b, n, nat.ptr(action), nat.ptr(demand), nat.ptr(used),
                  nat.ptr(used_out), nat.ptr(vcap), nat.ptr(visited), nat.ptr(visited_out),
-                 nat.ptr(cur), nat.ptr(done), nat.ptr(reward), nat.ptr(mask), None, None,
-                 nat.stream_of(demand))
+                 nat.ptr(cur), nat.ptr(done), nat.ptr(reward), nat.ptr(mask), None, None, s)
         lb = self._known_lb(td["visited"])
         if lb is not None:  # a step marks at most one more node visited
             self._remember_lb(visited_out, lb - 1)

@@ -147,15 +147,15 @@ class SLAPEnv(RL4COEnvBase):
         b, l = mask.shape
         p = td["freq"].shape[-2]
         dev = mask.device
-        assign_out = torch.empty_like(assign)
-        mask_out = torch.empty_like(mask)
-        i_out = torch.empty_like(i)
-        done = torch.empty((b, 1), dtype=torch.bool, device=dev)
-        reward = torch.empty((b, 1), dtype=torch.bool, device=dev)
+        s = nat.stream_of(mask)
+        assign_out = self._out(assign.shape, assign.dtype, dev, s)
+        mask_out = self._out(mask.shape, mask.dtype, dev, s)
+        i_out = self._out(i.shape, i.dtype, dev, s)
+        done = self._out((b, 1), torch.bool, dev, s)
+        reward = self._out((b, 1), torch.bool, dev, s)
         nat.call("co_slap_step", b, l, p, nat.ptr(action), nat.ptr(tc), tc.stride(0),
                  nat.ptr(assign), nat.ptr(assign_out), nat.ptr(mask), nat.ptr(mask_out),
-                 nat.ptr(i), nat.ptr(i_out), nat.ptr(done), nat.ptr(reward), None,
-                 nat.stream_of(mask))
+                 nat.ptr(i), nat.ptr(i_out), nat.ptr(done), nat.ptr(reward), None, s)
         lb = self._known_lb(td["i"])
         if lb is not None:
             self._remember_lb(i_out, lb - 1)

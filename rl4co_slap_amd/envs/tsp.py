@@ -83,14 +83,15 @@ class TSPEnv(RL4COEnvBase):
         if first_in is None:
             first_in = action
         first_in = first_in.contiguous()
-        mask_out = torch.empty_like(mask)
-        i_out = torch.empty_like(i)
-        first_out = torch.empty_like(action)
-        done = torch.empty(b, dtype=torch.bool, device=dev)
-        reward = torch.empty(b, dtype=torch.bool, device=dev)
+        s = nat.stream_of(mask)
+        mask_out = self._out(mask.shape, mask.dtype, dev, s)
+        i_out = self._out(i.shape, i.dtype, dev, s)
+        first_out = self._out(action.shape, torch.int64, dev, s)
+        done = self._out((b,), torch.bool, dev, s)
+        reward = self._out((b,), torch.bool, dev, s)
         nat.call("co_tsp_step", b, n, nat.ptr(action), nat.ptr(mask), nat.ptr(mask_out),
                  nat.ptr(i), nat.ptr(i_out), nat.ptr(first_in), nat.ptr(first_out), None,
-                 nat.ptr(done), nat.ptr(reward), mode, nat.ptr(flag), None, nat.stream_of(mask))
+                 nat.ptr(done), nat.ptr(reward), mode, nat.ptr(flag), None, s)
         if known is not None:
             self._remember_i(i_out, known + 1)
         lb = self._known_lb(td["action_mask"])
@@ -125,18 +126,20 @@ class TSPEnv(RL4COEnvBase):
         mask, i = mask.contiguous(), i.contiguous()
         first_in = first_in.contiguous() if (first_in is not None and not take) else None
         ain = action_in.long().contiguous() if action_in is not None else None
+        s = nat.stream_of(mask)
+        # the decoding strategy keeps every action and log-probability: never pooled
         act = torch.empty(b, dtype=torch.int64, device=dev)
         logp = torch.empty(b, dtype=torch.float32, device=dev)
-        mask_out = torch.empty_like(mask)
-        i_out = torch.empty_like(i)
-        first_out = torch.empty(b, dtype=torch.int64, device=dev)
-        done = torch.empty(b, dtype=torch.bool, device=dev)
-        reward = torch.empty(b, dtype=torch.bool, device=dev)
+        mask_out = self._out(mask.shape, mask.dtype, dev, s)
+        i_out = self._out(i.shape, i.dtype, dev, s)
+        first_out = self._out((b,), torch.int64, dev, s)
+        done = self._out((b,), torch.bool, dev, s)
+        reward = self._out((b,), torch.bool, dev, s)
         nat.call("co_tsp_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
                  float(tanh_clipping), float(temperature), mode, nat.ptr(ain), nat.ptr(act),
                  nat.ptr(logp), seed, offset, nat.ptr(mask_out), nat.ptr(i), nat.ptr(i_out),
                  nat.ptr(first_in), nat.ptr(first_out), take, nat.ptr(done), nat.ptr(reward),
-                 None, nat.ptr(status), nat.stream_of(mask))
+                 None, nat.ptr(status), s)
         sel = action_in if action_in is not None else act
         self._remember_i(i_out, known + 1)
         lb = self._known_lb(td["action_mask"])

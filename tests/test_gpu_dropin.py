@@ -186,3 +186,48 @@ def test_fused_decode_env_step_equals_two_launches(dev, monkeypatch, decode_type
     assert torch.equal(a["actions"], b_["actions"])
     assert torch.equal(a["log_likelihood"], b_["log_likelihood"])
     assert torch.equal(a["reward"], b_["reward"])
+
+
+@pytest.mark.parametrize("name", ["tsp", "cvrp", "slap"])
+def test_pooled_step_outputs_never_overwrite_held_tensors(dev, name):
+    """envs/base.py `_out`: a step's outputs come from the env's pool only when nothing
+    else refers to a pooled tensor.  Every tensor a caller keeps -- whole TensorDicts,
+    single entries, views -- must keep the value it had when its step returned, and a
+    loop that keeps nothing reuses the same few buffers."""
+    from rl4co_slap_amd.envs import SLAPEnv
+
+    env = {"tsp": TSPEnv, "cvrp": CVRPEnv, "slap": SLAPEnv}[name](device=dev)
+    n_steps = 12
+
+    def rollout(keep):
+        torch.manual_seed(3)
+        td = env.reset(batch_size=[32])
+        held, ids = [], set()
+        for t in range(n_steps):
+            mask = td["action_mask"]
+            action = torch.multinomial(mask.float() + 1e-9 * (~mask).float(), 1).squeeze(1)
+            td.set("action", action)
+            td = env.step(td)["next"]
+            ids.add(id(td["action_mask"]))
+            if keep == "entries":
+                held.append({k: (td[k], td[k].clone()) for k in ("action_mask", "done", "i")
+                             if k in td.keys()})
+            elif keep == "views":
+                held.append({"action_mask": (td["action_mask"][1:], td["action_mask"][1:].clone())})
+            elif keep == "tds":
+                held.append({k: (td[k], td[k].clone()) for k in td.keys()
+                             if isinstance(td[k], torch.Tensor)})
+        torch.cuda.synchronize()
+        return held, ids
+
+    for keep in ("entries", "views", "tds"):
+        held, _ = rollout(keep)
+        for t, rec in enumerate(held):
+            for k, (x, snap) in rec.items():
+                assert torch.equal(x, snap), (keep, t, k)
+    del held, rec, x, snap
+    env._pool.clear()
+    _, ids = rollout(None)
+    # every mask the loop saw was one of the pool's own (live) tensors
+    slots = [t for lst in env._pool._slots.values() for t in lst]
+    assert ids <= {id(t) for t in slots} and len(ids) <= 2, len(ids)

@@ -14,7 +14,7 @@ from rl4co_slap_amd.envs import TSPEnv  # noqa: E402
 from rl4co_slap_amd.rollout.constructive import ConstructivePolicy, LogitsDecoder  # noqa: E402
 from rl4co_slap_amd.td import TensorDict  # noqa: E402
 
-dev = torch.device("cuda:0")
+dev = torch.device(os.environ.get("CO_DEV", "cuda:0"))  # CO_DEV=cpu: the host build
 b, n = 64, 100
 locs = torch.rand(b, n, 2, device=dev)
 logits = torch.randn(b, n, device=dev)
@@ -25,7 +25,8 @@ pol = ConstructivePolicy(None, LogitsDecoder(lambda td: logits), env_name="tsp")
 def run(k):
     for _ in range(k):
         pol(env.reset(TensorDict({"locs": locs}, [b])), env, phase="test", decode_type="greedy")
-    torch.cuda.synchronize()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
 
 
 run(3)
