@@ -76,6 +76,16 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
 #define CO_TSP_STEP_GROUP 1
 #endif
 
+#ifndef CO_TSP_WPL
+#define CO_TSP_WPL 4
+#endif
+#ifndef CO_TSP_LAYOUT
+#define CO_TSP_LAYOUT 1
+#endif
+#ifndef CO_TSP_SCUT
+#define CO_TSP_SCUT 0  // timing diagnostic only: 1 no row epilogue, 2 no mask store
+#endif
+
 template <int G>
 __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
                                                              const int64_t* __restrict__ action,
@@ -84,7 +94,7 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
                                                              TspRowEpilogue epi, int first_mode,
                                                              const int32_t* first_flag,
                                                              int32_t* status) {
-  constexpr int WPL = 4;
+  constexpr int WPL = CO_TSP_WPL;
   const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
   const int W = N >> 2;  // words per row
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -97,23 +107,37 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
     const int64_t r = valid ? b : 0;
     const int64_t a_raw = action[r];
     int64_t a = a_raw;
-    const typename TspRowEpilogue::Row rv = valid ? epi.load(r) : typename TspRowEpilogue::Row{};
+    // row scalars: with G >= 8 spread over the group's lanes (lane 0 reads i, lane 1
+    // first_node: one load instruction; lanes 0-2 write i / first / current: one 8-B
+    // store; lanes 3, 4 done / reward: one byte store), else lane 0 does all of them
+    typename TspRowEpilogue::Row rv{};
+    int64_t rs = 0;
+    if constexpr (G >= 8) {
+      const int64_t* rsrc = sl == 0 ? epi.i_in : epi.first_in;
+      if (valid && (sl == 0 || (sl == 1 && !epi.take_first)) && !(CO_TSP_SCUT & 1)) rs = rsrc[r];
+    } else if (valid && !(CO_TSP_SCUT & 1)) {
+      rv = epi.load(r);
+    }
     const uint32_t* src = mask_in + r * W;
     uint32_t w[WPL];
+    // CO_TSP_LAYOUT 1: word c = sl + k*G (each load/store instruction covers G consecutive
+    // words of a row); 0: c = sl*WPL + k (a lane's words adjacent)
+#define CO_TSP_WORD(k) (CO_TSP_LAYOUT ? sl + (k) * G : sl * WPL + (k))
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
-      const int c = sl * WPL + k;
+      const int c = CO_TSP_WORD(k);
       w[k] = (valid && c < W) ? src[c] : 0u;
     }
     if (a < 0 || a >= N) {
       if (valid && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
       a = -1;
     }
-    const int rel = (int)a - sl * WPL * 4;  // byte offset of the action in this lane's span
+    const int aw = a >= 0 ? (int)(a >> 2) : -1;  // the action's word and byte
+    const uint32_t aclr = 0xffu << (8 * (int)(a & 3));
     int left = 0;
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
-      const uint32_t clr = (rel >= 4 * k && rel < 4 * k + 4) ? (0xffu << (8 * (rel - 4 * k))) : 0u;
+      const uint32_t clr = CO_TSP_WORD(k) == aw ? aclr : 0u;
       w[k] &= ~clr;
       // nonzero bytes of the word: high bit of each byte of (b & 0x7f) + 0x7f, or b
       const uint32_t nz = (((w[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[k]) & 0x80808080u;
@@ -122,11 +146,21 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
     uint32_t* dst = mask_out + r * W;
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
-      const int c = sl * WPL + k;
-      if (valid && c < W) dst[c] = w[k];
+      const int c = CO_TSP_WORD(k);
+      if (valid && c < W && !(CO_TSP_SCUT & 2)) dst[c] = w[k];
     }
+#undef CO_TSP_WORD
     const bool any_left = (__ballot(left != 0) & gmask) != 0;
-    if (valid && sl == 0) epi.store(r, a_raw, any_left ? 1 : 0, rv);
+    if constexpr (G >= 8) {
+      if (valid && !(CO_TSP_SCUT & 1)) {
+        int64_t* d8 = sl == 0 ? epi.i_out : sl == 1 ? epi.first_out : epi.cur_out;
+        const int64_t v8 = sl == 0 ? rs + 1 : (sl == 1 && !epi.take_first) ? rs : a_raw;
+        if (sl < 3 && d8) d8[r] = v8;
+        if (sl == 3 || sl == 4) (sl == 3 ? epi.done : epi.reward)[r] = sl == 3 ? !any_left : 0;
+      }
+    } else if (valid && sl == 0 && !(CO_TSP_SCUT & 1)) {
+      epi.store(r, a_raw, any_left ? 1 : 0, rv);
+    }
   }
 }
 
@@ -235,10 +269,10 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
   const int vec = tile_vec_ok(mask_in, mask_out);
   TspRowEpilogue epi{i_in, i_out, first_in, first_out, current_out, done, reward,
                      first_mode == 1};
-  if (CO_TSP_STEP_GROUP && (N & 3) == 0 && N <= 1024 &&
+  if (CO_TSP_STEP_GROUP && (N & 3) == 0 && (N >> 2) <= 64 * CO_TSP_WPL &&
       ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) & 3) == 0) {
-    const int W = (int)(N >> 2), G = W <= 8 ? 2 : W <= 16 ? 4 : W <= 32 ? 8 : W <= 64 ? 16
-                                                             : W <= 128 ? 32 : 64;
+    const int W = (int)(N >> 2), WG = (W + CO_TSP_WPL - 1) / CO_TSP_WPL;
+    const int G = WG <= 2 ? 2 : WG <= 4 ? 4 : WG <= 8 ? 8 : WG <= 16 ? 16 : WG <= 32 ? 32 : 64;
     const int64_t waves = (B * G + 63) / 64;
     const dim3 grid(grid_for(waves, 4, 256 * 32));
     const uint32_t* mi = reinterpret_cast<const uint32_t*>(mask_in);
