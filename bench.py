@@ -476,9 +476,9 @@ def main():
         modes["dropin_tsp100"] = bench_dropin(b, n, k, world, rank, dev)
         # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
         modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
-        # the north star's "SLAP at batch 65,536" (fused episode only)
+        # the north star's "SLAP at batch 65,536": fused and stepwise
         modes.update({k2 + "_b65536": v for k2, v in
-                      bench_slap(65536, k, world, rank, dev, stepwise=False).items()})
+                      bench_slap(65536, k, world, rank, dev).items()})
         # POMO TSP-100 (config 5): 1,024 instances x 100 starts per GPU, decode-fused steps
         # on HBM-resident logits, shared baseline + RCCL all-gather of per-instance results
         modes["pomo_tsp100"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev)
@@ -570,6 +570,8 @@ def annotate_modes(modes, n, world):
         "slap_fused_random_b65536": lambda m: 2354 / 20,
         "slap_stepwise_graph": lambda m: 234 + 1684 / 20,
         "slap_stepwise_graph_teacher": lambda m: 234 + 1684 / 20,
+        "slap_stepwise_graph_b65536": lambda m: 234 + 1684 / 20,
+        "slap_stepwise_graph_teacher_b65536": lambda m: 234 + 1684 / 20,
         "pomo_tsp100": lambda m: 6 * n + 54,
         "pomo_tsp100_fast_math": lambda m: 6 * n + 54,
         "pomo_tsp100_certified": lambda m: 6 * n + 54,

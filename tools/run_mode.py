@@ -32,7 +32,7 @@ def main():
     elif a.mode == "slap":
         out = bench.bench_slap(16384, a.k, 1, 0, dev)
     elif a.mode == "slap65k":
-        out = bench.bench_slap(65536, a.k, 1, 0, dev, stepwise=False)
+        out = bench.bench_slap(65536, a.k, 1, 0, dev)
     elif a.mode == "steps":
         out = bench.step_kernels_vs_copy(dev)
         out = {k: round(v["kernel_us"], 3) for k, v in out.items()}
