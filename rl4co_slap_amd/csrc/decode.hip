@@ -53,6 +53,9 @@ __device__ __forceinline__ float co_exp_fast(float x) { return co_exp2(x * 1.442
 // (GreedyRow kernels only, CO_DECODE_CERTIFIED: fast math, then the exact recomputation
 // for every wave holding a row whose fast argmax the error bound cannot certify)
 constexpr int kOptClip = 1, kOptTemp = 2, kOptFast = 4, kOptCert = 8;
+#ifndef CO_TANH_COMPACT
+#define CO_TANH_COMPACT 1  // GreedyRow: exact tanh of allowed elements only, wave-compacted
+#endif
 
 template <int OPT>
 __device__ __forceinline__ float clip_tanh(float x) {
@@ -432,15 +435,57 @@ struct GreedyRow {
   // leaves v[k] = x_k - m; returns L (NaN for the degenerate rows above)
   // OPT bit 0: tanh clipping, bit 1: temperature != 1 (template flags: as runtime
   // conditions the compiler evaluates both arms per element and selects)
+  // Exact tanh of the row's allowed elements only (a masked element becomes -inf whatever
+  // its tanh), wave-compacted: the allowed raw logits of the wave's rows are packed into
+  // the wave's LDS scratch (ballot + mbcnt positions per element slot), every lane takes
+  // every 64th packed entry, and the results go back to their slots.  The f64 tanh runs
+  // ceil(allowed / 64) times per wave instead of EPL times -- about half as often over a
+  // TSP episode -- with the same bits per element.  All lanes of the wave must be active.
+  __device__ __forceinline__ void tanh_allowed_compact(float* wave_lds) {
+    const int lane = lane_id();
+    int pos[EPL], total = 0;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const bool a = allowed(k);
+      const uint64_t bal = __ballot(a);
+      pos[k] = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+      if (a) wave_lds[pos[k]] = v[k];
+      total += __popcll(bal);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int j = lane; j < total; j += 128) {  // two independent f64 chains per lane
+      const bool two = j + 64 < total;
+      const float x0 = wave_lds[j], x1 = two ? wave_lds[j + 64] : 0.f;
+      const float y0 = tanh_cr(x0), y1 = tanh_cr(x1);
+      wave_lds[j] = y0;
+      if (two) wave_lds[j + 64] = y1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < EPL; ++k)
+      if (allowed(k)) v[k] = wave_lds[pos[k]];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the reads above stay before the scratch's next writes
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+
   template <int OPT>
   __device__ __forceinline__ float softmax_shift(float clip, float temp, int N, int sl,
                                                  float* lds_row) {
     const float NEG_INF = -__builtin_inff();
+    // exact tanh clipping: tanh of the allowed elements, wave-compacted (above)
+    constexpr bool kCompact = (OPT & kOptClip) && !(OPT & kOptFast) && CO_TANH_COMPACT;
+    if constexpr (kCompact) tanh_allowed_compact(lds_row - (lane_id() / RL) * (RL * EPL));
     float m = NEG_INF;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
       float t = v[k];
-      if (OPT & kOptClip) t = clip_tanh<OPT>(t) * clip;
+      if (OPT & kOptClip) t = (kCompact ? t : clip_tanh<OPT>(t)) * clip;
       if (OPT & kOptTemp) t = t / temp;
       t = allowed(k) ? t : NEG_INF;
       v[k] = t;

@@ -111,6 +111,37 @@ def test_tsp_fused_large_batch_invalid_tour_flag(dev, bad):
     assert ((got - ref).abs() <= 1e-5 * ref.abs().clamp(min=1)).all()
 
 
+@pytest.mark.parametrize("b", [768 * 64 + 40, 65536, 2 * 768 * 64 + 100])
+def test_tsp_fused_split_tail_tiles_final_state(dev, b):
+    """Batches past one resident round (768 full 64-instance tiles on 256 CUs) end in
+    split tiles (32 instances, 8 step ranges).  Every row's final state and reward against
+    the reference semantics computed on the CPU: mask = nodes absent from the action row
+    (rows with a revisit keep one), done = nothing left, first / current node, i = N."""
+    from oracle.ops import gather_by_index, get_tour_length
+
+    n = 100
+    g = torch.Generator().manual_seed(b)
+    locs = torch.rand(b, n, 2, generator=g)
+    acts = torch.rand(b, n, generator=g).argsort(1)
+    bad = torch.tensor([0, 49151, 49152, 49183, 49184, b - 1])
+    acts[bad, 50] = acts[bad, 10]  # a revisit: the node at step 50 is never visited
+    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep.run_eager()
+    torch.cuda.synchronize()
+    st = ep.final_state()
+    assert int(ep.status.item()) & 1
+    left = torch.ones(b, n, dtype=torch.bool)
+    left.scatter_(1, acts, False)
+    assert torch.equal(st["action_mask"].cpu(), left)
+    assert torch.equal(st["done"].cpu().view(-1), ~left.any(1))
+    assert (st["i"].cpu() == n).all()
+    assert torch.equal(st["first_node"].cpu().view(-1), acts[:, 0])
+    assert torch.equal(st["current_node"].cpu().view(-1), acts[:, -1])
+    ref = -get_tour_length(gather_by_index(locs, acts))
+    got = st["reward"].cpu().view(-1)
+    assert ((got - ref).abs() <= 1e-5 * ref.abs().clamp(min=1)).all()
+
+
 def _slap_ref(b, seed, policy):
     import numpy as np
 
