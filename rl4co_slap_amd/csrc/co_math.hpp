@@ -116,6 +116,10 @@ __device__ __forceinline__ float aten_logf(float d) {
 // ~30 f64 operations against ~140 for the libm tanh(double) (double-double inside).
 // |x| < 2^-12 returns x (tanh x = x(1 - x^2/3 ...) rounds to x there) and |x| >= 9.1 returns
 // +-1 (tanh rounds to 1 from 9.0109); NaN propagates.
+__device__ __forceinline__ double sconst(double c) {
+  asm volatile("" : "+s"(c));  // a scalar register here: SALU moves, not a live VGPR pair
+  return c;
+}
 __device__ __forceinline__ float tanh_cr(float x) {
   const float ax = __builtin_fabsf(x);
   if (!(ax >= 0x1p-12f)) return x;            // tiny, or NaN
@@ -125,17 +129,20 @@ __device__ __forceinline__ float tanh_cr(float x) {
   const int k = (int)kd;
   double r = __builtin_fma(kd, -6.93147180559890330187e-01, y);   // ln2 hi (exact product)
   r = __builtin_fma(kd, -5.49792301870837115524e-14, r);          // ln2 lo
-  double q = 1.0 / 6227020800.0;                                  // 1/13!
-  q = __builtin_fma(q, r, 1.0 / 479001600.0);
-  q = __builtin_fma(q, r, 1.0 / 39916800.0);
-  q = __builtin_fma(q, r, 1.0 / 3628800.0);
-  q = __builtin_fma(q, r, 1.0 / 362880.0);
-  q = __builtin_fma(q, r, 1.0 / 40320.0);
-  q = __builtin_fma(q, r, 1.0 / 5040.0);
-  q = __builtin_fma(q, r, 1.0 / 720.0);
-  q = __builtin_fma(q, r, 1.0 / 120.0);
-  q = __builtin_fma(q, r, 1.0 / 24.0);
-  q = __builtin_fma(q, r, 1.0 / 6.0);
+  // the Taylor coefficients are materialised into SGPRs at each use (sconst): hoisted out
+  // of the kernels' loops they occupied 20 VGPRs for the whole kernel, plus a register
+  // copy per Horner step (v_fmac accumulates into its constant's register)
+  double q = sconst(1.0 / 6227020800.0);                          // 1/13!
+  q = __builtin_fma(q, r, sconst(1.0 / 479001600.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 39916800.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 3628800.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 362880.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 40320.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 5040.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 720.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 120.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 24.0));
+  q = __builtin_fma(q, r, sconst(1.0 / 6.0));
   q = __builtin_fma(q, r, 0.5);
   const double p = __builtin_fma(r * r, q, r);                    // expm1(r)
   // expm1(y) = 2^k p + (2^k - 1), both terms exact-scaled; k <= 0

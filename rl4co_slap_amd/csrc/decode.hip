@@ -56,6 +56,9 @@ constexpr int kOptClip = 1, kOptTemp = 2, kOptFast = 4, kOptCert = 8;
 #ifndef CO_TANH_COMPACT
 #define CO_TANH_COMPACT 1  // GreedyRow: exact tanh of allowed elements only, wave-compacted
 #endif
+#ifndef CO_TANH_CHAINS
+#define CO_TANH_CHAINS 2  // packed tanh evaluations per lane and loop iteration (1 or 2)
+#endif
 
 template <int OPT>
 __device__ __forceinline__ float clip_tanh(float x) {
@@ -456,6 +459,7 @@ struct GreedyRow {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if CO_TANH_CHAINS == 2
     for (int j = lane; j < total; j += 128) {  // two independent f64 chains per lane
       const bool two = j + 64 < total;
       const float x0 = wave_lds[j], x1 = two ? wave_lds[j + 64] : 0.f;
@@ -463,6 +467,9 @@ struct GreedyRow {
       wave_lds[j] = y0;
       if (two) wave_lds[j + 64] = y1;
     }
+#else
+    for (int j = lane; j < total; j += 64) wave_lds[j] = tanh_cr(wave_lds[j]);
+#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -474,12 +481,14 @@ struct GreedyRow {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 
-  template <int OPT>
+  // COMPACT = false: the certified path's rare exact fallback (the compaction there made
+  // the whole certified kernel slower: 2.09 -> 2.37 ms per POMO episode)
+  template <int OPT, bool COMPACT = true>
   __device__ __forceinline__ float softmax_shift(float clip, float temp, int N, int sl,
                                                  float* lds_row) {
     const float NEG_INF = -__builtin_inff();
     // exact tanh clipping: tanh of the allowed elements, wave-compacted (above)
-    constexpr bool kCompact = (OPT & kOptClip) && !(OPT & kOptFast) && CO_TANH_COMPACT;
+    constexpr bool kCompact = COMPACT && (OPT & kOptClip) && !(OPT & kOptFast) && CO_TANH_COMPACT;
     if constexpr (kCompact) tanh_allowed_compact(lds_row - (lane_id() / RL) * (RL * EPL));
     float m = NEG_INF;
 #pragma unroll
@@ -559,7 +568,7 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
     if (__any(!ok)) {  // rare: the exact evaluation for the whole wave
 #pragma unroll
       for (int k = 0; k < EPL; ++k) g.v[k] = raw[k];
-      L = g.template softmax_shift<OE>(clip, temp, N, sl, lds_row);
+      L = g.template softmax_shift<OE, false>(clip, temp, N, sl, lds_row);
       sel = g.select(L, c0, lp);
     }
     return sel;
