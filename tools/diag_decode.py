@@ -12,7 +12,11 @@ if os.environ.get("DIAG_LIB"):
 print("lib:", nat.LIB_PATH)
 nat.load()
 dev = torch.device("cuda:0")
-for B, N in [(102400, 100), (65536, 100), (102400, 20), (102400, 50), (16384, 200)]:
+BASE_MODE = int(os.environ.get("DIAG_DECODE_MODE", "0"))  # 0 greedy, 1 sampling, 2 evaluate
+SIZES = [(102400, 100), (65536, 100), (102400, 20), (102400, 50), (16384, 200)]
+if os.environ.get("DIAG_SIZES") == "tsp100":
+    SIZES = [(102400, 100)]
+for B, N in SIZES:
     logits = torch.randn(B, N, device=dev)
     mask = torch.rand(B, N, device=dev) > 0.3
     mask[:, 0] = True
@@ -31,10 +35,10 @@ for B, N in [(102400, 100), (65536, 100), (102400, 20), (102400, 50), (16384, 20
         for name in ("decode", "tsp_decode"):
             def run():
                 if name == "decode":
-                    nat.call("co_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, fast,
+                    nat.call("co_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, BASE_MODE | fast,
                              None, nat.ptr(out_a), nat.ptr(lp), None, 0, 0, nat.ptr(st), s)
                 else:
-                    nat.call("co_tsp_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, fast,
+                    nat.call("co_tsp_decode_step", B, N, nat.ptr(logits), N, nat.ptr(mask), clip, 1.0, BASE_MODE | fast,
                              None, nat.ptr(out_a), nat.ptr(lp), 0, 0, nat.ptr(m2), nat.ptr(i0),
                              nat.ptr(i1), nat.ptr(f0), nat.ptr(f1), 0, nat.ptr(done), nat.ptr(sr),
                              None, nat.ptr(st), s)
@@ -60,5 +64,5 @@ for B, N in [(102400, 100), (65536, 100), (102400, 20), (102400, 50), (16384, 20
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / 50
             byts = B * (5 * N + 16) if name == "decode" else B * (6 * N + 54)
-            print(f"B={B} N={N} clip={clip} fast={bool(fast)} {name}: {us:.1f} us  "
+            print(f"mode={BASE_MODE} B={B} N={N} clip={clip} fast={bool(fast)} {name}: {us:.1f} us  "
                   f"{byts / us / 1e3:.0f} GB/s", flush=True)
