@@ -66,11 +66,25 @@ __device__ __forceinline__ void copy_tile_out(const unsigned char* scratch, int 
   for (int k = n16 + tid; k < nbytes; k += blockDim.x) dst[k] = scratch[k];
 }
 
+// The whole block writes zeros over a tile of mask bytes (16-byte stores when aligned).
+__device__ __forceinline__ void zero_tile_out(int nbytes, uint8_t* __restrict__ dst) {
+  const int tid = threadIdx.x;
+  const int n16 = ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) ? (nbytes & ~15) : 0;
+  for (int off = tid * 16; off < n16; off += blockDim.x * 16)
+    *reinterpret_cast<uint4*>(dst + off) = make_uint4(0u, 0u, 0u, 0u);
+  for (int k = n16 + tid; k < nbytes; k += blockDim.x) dst[k] = 0;
+}
+
+#ifndef CO_TEACH_ZFAST
+#define CO_TEACH_ZFAST 1  // all-visited tiles store zero mask rows without the LDS expansion
+#endif
+
 // LDS bytes of the TSP teacher kernel's coordinate tile region: [64][N] float2, or the
 // post-episode scratch (mask bytes, Q x 64 partial sums, last node) if larger.
 __host__ __device__ inline size_t tsp_tile_bytes(int N, int Q) {
   const size_t xy = (size_t)64 * N * 8;
-  const size_t scr = (((size_t)64 * N + 15) & ~(size_t)15) + (size_t)Q * 64 * 8 + 64 * 8 + 64 * 4;
+  const size_t scr = (((size_t)64 * N + 15) & ~(size_t)15) + (size_t)Q * 64 * 8 + 64 * 8 + 64 * 4 +
+                     16 * 4;  // + per-wave "all visited" flags
   return ((xy > scr ? xy : scr) + 15) & ~(size_t)15;
 }
 
@@ -240,13 +254,32 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
   uint64_t m[NW];
 #pragma unroll
   for (int kk = 0; kk < NW; ++kk) m[kk] = (uint64_t)vw[2 * kk] | ((uint64_t)vw[2 * kk + 1] << 32);
-  if (STATE && live) {  // the Q waves expand column quarters of the lane's mask row
-    const int per = ((N + 4 * Q - 1) / (4 * Q)) * 4;
-    const int c_lo = q * per < N ? q * per : N;
-    const int c_hi = c_lo + per < N ? c_lo + per : N;
-    mask_row_to_lds<NW>(m, N, smem + (size_t)lane * N, c_lo, c_hi);
+  bool empty = true;
+#pragma unroll
+  for (int kk = 0; kk < NW; ++kk) empty &= (m[kk] == 0);
+  // Every instance of the tile fully visited (any valid tour): its mask rows are all zero
+  // and are stored as zeros, without the LDS expansion and its read-back.
+  int* s_flag = s_lasta + 64;  // [Q]
+  bool all_empty = false;
+  if (STATE && CO_TEACH_ZFAST) {
+    const bool wave_empty = __ballot(live && !empty) == 0ull;
+    if (lane == 0) s_flag[q] = wave_empty;
+    __syncthreads();
+    all_empty = true;
+#pragma unroll
+    for (int w = 0; w < Q; ++w) all_empty &= s_flag[w] != 0;
   }
-  __syncthreads();
+  if (STATE && !all_empty) {
+    if (live) {  // the Q waves expand column quarters of the lane's mask row
+      const int per = ((N + 4 * Q - 1) / (4 * Q)) * 4;
+      const int c_lo = q * per < N ? q * per : N;
+      const int c_hi = c_lo + per < N ? c_lo + per : N;
+      mask_row_to_lds<NW>(m, N, smem + (size_t)lane * N, c_lo, c_hi);
+    }
+    __syncthreads();
+  } else if (!STATE) {
+    __syncthreads();
+  }
   if (q == 0 && live) {
     double tot = 0.0;
 #pragma unroll
@@ -256,9 +289,6 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
     tot += (double)edge_len(pl.x, pl.y, fx, fy);  // closing edge (roll by -1)
     reward_out[b] = -(float)tot;
     if (STATE) {
-      bool empty = true;
-#pragma unroll
-      for (int kk = 0; kk < NW; ++kk) empty &= (m[kk] == 0);
       first_out[b] = first;
       cur_out[b] = s_lasta[lane];
       i_out[b] = N;
@@ -266,7 +296,12 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
       step_reward_out[b] = 0;
     }
   }
-  if (STATE) copy_tile_out(smem, rows * N, mask_out + row0 * N);
+  if (STATE) {
+    if (all_empty)
+      zero_tile_out(rows * N, mask_out + row0 * N);
+    else
+      copy_tile_out(smem, rows * N, mask_out + row0 * N);
+  }
 }
 
 // ascending sort of EPL u64 keys in registers (Batcher odd-even merge network)
