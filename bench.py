@@ -445,6 +445,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "tsp_teacher_kernel<2,4,true> (co_tsp_rollout)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     # the same bytes over the wall time `value` uses (launch gaps included)
+                     "achieved_wall": bytes_per_launch / (t / args.steps) / 1e9,
+                     "frac_wall": bytes_per_launch / (t / args.steps) / 1e9 / HBM_PEAK_GBS,
                      "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "launch_us": per_launch * 1e6,
                      "copy_probe": copy_probe(bytes_per_launch, dev, args.steps)},
@@ -481,13 +484,14 @@ def main():
                       bench_slap(65536, k, world, rank, dev).items()})
         # POMO TSP-100 (config 5): 1,024 instances x 100 starts per GPU, decode-fused steps
         # on HBM-resident logits, shared baseline + RCCL all-gather of per-instance results
+        # default decode math = certified (exact greedy actions, logp within 1e-5)
         modes["pomo_tsp100"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev)
-        # the same with the opt-in CO_DECODE_FAST math (not bit-exact; reported separately)
+        # the ATen-exact math (log-probabilities bit for bit; opt-in, decode_math="exact")
+        modes["pomo_tsp100_exact"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev,
+                                                decode_math="exact")
+        # the opt-in CO_DECODE_FAST math (not bit-exact; reported separately)
         modes["pomo_tsp100_fast_math"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev,
-                                                    fast_math=True)
-        # certified greedy: exact actions at close to the fast-math speed
-        modes["pomo_tsp100_certified"] = bench_pomo(1024, n, max(2, k // 2), world, rank, dev,
-                                                    certified=True)
+                                                    decode_math="fast")
         # CVRP-100 (config 3), nearest-feasible policy: fused episode and stepwise loop
         modes.update(bench_cvrp(32768, 100, k, world, rank, dev))
         # instance generation, timed separately (SURVEY.md 8d protocol; 8f rank 1)
@@ -574,7 +578,7 @@ def annotate_modes(modes, n, world):
         "slap_stepwise_graph_teacher_b65536": lambda m: 234 + 1684 / 20,
         "pomo_tsp100": lambda m: 6 * n + 54,
         "pomo_tsp100_fast_math": lambda m: 6 * n + 54,
-        "pomo_tsp100_certified": lambda m: 6 * n + 54,
+        "pomo_tsp100_exact": lambda m: 6 * n + 54,
         "cvrp_fused_nearest": lambda m: (8 + 12 * n + 8 * m["episode_steps"] + 10 * (n + 1) + 25)
         / m["episode_steps"],
         # fused policy: locs 8(N+1) + mask, visited N+1 each + demand 4N + 16 B state read;
@@ -851,16 +855,17 @@ def bench_generate_uniform(b, n, dev, reps=5):
     return out
 
 
-def bench_pomo(b, n, k, world, rank, dev, fast_math=False, certified=False):
+def bench_pomo(b, n, k, world, rank, dev, decode_math=None):
     from rl4co_slap_amd.rollout.pomo import POMOEpisode, global_metrics
+    from rl4co_slap_amd.utils.decoding import default_decode_math
 
     torch.manual_seed(1234 + rank)
     locs = torch.rand(b, n, 2).to(dev)
     e = b * n
     g = torch.Generator(device=dev).manual_seed(99 + rank)
     logits = torch.randn((n - 1, e, n), generator=g, device=dev)  # policy-network stand-in
-    ep = POMOEpisode(locs, logits, tanh_clipping=10.0, fast_math=fast_math,
-                     certified=certified).capture()
+    ep = POMOEpisode(locs, logits, tanh_clipping=10.0, decode_math=decode_math).capture()
+    decode_math = ep.decode_math
 
     def run():
         ep.replay()
@@ -868,24 +873,28 @@ def bench_pomo(b, n, k, world, rank, dev, fast_math=False, certified=False):
     wall, ev = timed(run, k, 1, world, dev)
     assert int(ep.status.item()) == 0
     t = max_over_ranks(wall, world, dev)
-    m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n)  # warm-up (communicator setup)
+    total = world * b  # every rank holds b instances: shard sizes known, one all-gather
+    m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n,
+                       total_instances=total)  # warm-up (communicator setup)
     ag = []
     for _ in range(10):  # the RCCL exchange itself (no collective at world size 1)
         torch.cuda.synchronize(dev)
         barrier(world)
         t0 = time.perf_counter()
-        m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n)
+        m = global_metrics(ep.bl, ep.max_reward, ep.loss_terms, n, total_instances=total)
         torch.cuda.synchronize(dev)
         ag.append(time.perf_counter() - t0)
     t_ag = sorted(ag)[len(ag) // 2]
     return {"value": world * e * n * k / t, "ms_per_episode": t / k * 1e3,
             "instances_per_gpu": b, "starts": n, "envs_per_gpu": e,
             "bytes_per_env_step_decode_fused": 6 * n + 54,
-            "decode_math": "fast (CO_DECODE_FAST, opt-in, not bit-exact)" if fast_math
-            else ("certified (CO_DECODE_CERTIFIED: greedy actions = the exact path's by a "
-                  "per-row error bound + exact recomputation of uncertified waves; logp fast, "
-                  "within ~1e-6)" if certified
-                  else "exact (ATen log_softmax bits, correctly rounded tanh)"),
+            "decode_math": {
+                "fast": "fast (CO_DECODE_FAST, opt-in, not bit-exact)",
+                "certified": "certified (the default; CO_DECODE_CERTIFIED: greedy actions = the "
+                             "exact path's by a per-row error bound + exact recomputation of "
+                             "uncertified waves; logp from the fast math, within 1e-5)",
+                "exact": "exact (opt-in; ATen log_softmax bits, correctly rounded tanh)",
+            }[decode_math],
             "allgather_ms": t_ag * 1e3,
             "allgather_note": "median of 10 after a warm-up call" + (
                 "" if world > 1 else "; world size 1: no collective runs, host bookkeeping only"),

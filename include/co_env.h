@@ -185,7 +185,8 @@ int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t* flag, voi
  * exp(logp) with a Philox draw keyed by (seed, offset, b); evaluate: action_in.
  * action_out[b], logp_sel[b] = logp[b, action]; logprobs_full (nullable)
  * receives the whole row.  Greedy/sampling picking a masked action sets
- * CO_ST_INFEASIBLE. */
+ * CO_ST_INFEASIBLE.  Rows of n_actions > 2048 run a workgroup-per-row kernel in the
+ * exact math whatever the math flags (top-p filtering is not offered there: CO_E_INVAL). */
 int co_decode_step(int64_t batch, int64_t n_actions, const float* logits, int64_t logits_stride,
                    const uint8_t* mask, float tanh_clipping, float temperature, int mode,
                    const int64_t* action_in, int64_t* action_out, float* logp_sel,
@@ -268,7 +269,10 @@ int co_slap_closest_step(int64_t batch, int64_t num_slots, int64_t n_products,
  * in-kernel policy, the actions.  Actions are step-major [N, B] (row t = the [B]
  * action tensor of step t).  acts_in != NULL: teacher-forced (Evaluate mode);
  * acts_in == NULL: nearest-unvisited policy (co_tsp_nearest_action) writing
- * acts_out.  check != 0: a non-permutation sets CO_ST_INVALID_TOUR.  N <= 256. */
+ * acts_out.  check != 0: a non-permutation sets CO_ST_INVALID_TOUR.  One launch for
+ * N <= 256 (teacher) / N <= 1024 (nearest); longer episodes run the same steps as a
+ * sequence of the stepwise kernels (co_tsp_reset, co_tsp_step in place, co_tsp_reward),
+ * with identical outputs. */
 int co_tsp_rollout(int64_t batch, int64_t num_loc, const float* locs, const int64_t* acts_in,
                    int64_t* acts_out, uint8_t* action_mask, int64_t* first_node,
                    int64_t* current_node, int64_t* i, uint8_t* done, uint8_t* step_reward,

@@ -210,37 +210,73 @@ def require_device(*tensors):
 
 
 _KIND = {_i64: "i", _i32: "i", _u64: "i", _p: "i", _f32: "f", _f64: "d"}
-_fast = None  # (invoke, {name: (address, kinds)}, {name: (address, kinds)}) once loaded
-FASTCALL_PATH = os.path.join(_HERE, "_lib", "_co_fastcall.so")
+
+
+def _fastcall_path() -> str:
+    """The fast-call module built for THIS interpreter (csrc/build.py names it with the
+    interpreter's EXT_SUFFIX, so a module built against other Python headers is never
+    picked up)."""
+    import sysconfig
+
+    return os.path.join(_HERE, "_lib", "_co_fastcall" + (sysconfig.get_config_var("EXT_SUFFIX")
+                                                         or ".so"))
+
+
+FASTCALL_PATH = _fastcall_path()
+
+
+class _FastCall:
+    """The CPython fast-call module (csrc/pycall/co_fastcall.cpp) and, per library, the
+    entry points' addresses and argument classes.  Each table is built on its first use,
+    so host-only callers never load the device library; any failure to load the module or
+    a library leaves that table empty and the call goes through ctypes."""
+
+    def __init__(self, invoke):
+        self.invoke = invoke
+        self._tables = {}
+
+    @staticmethod
+    def _table(lib, names):
+        return {n: (ctypes.cast(getattr(lib, n), ctypes.c_void_p).value,
+                    "".join(_KIND[t] for t in _SIGS[n]).encode()) for n in names}
+
+    def table(self, which):
+        t = self._tables.get(which)
+        if t is None:
+            try:
+                t = (self._table(load(), list(_SIGS)) if which == "dev"
+                     else self._table(load_host(), HOST_SYMBOLS))
+            except Exception:  # missing / unloadable library: ctypes raises the real error
+                t = {}
+            self._tables[which] = t
+        return t
+
+
+_fast = None  # a _FastCall once loaded, False when unavailable
 
 
 def _fastcall():
-    """The CPython fast-call module (csrc/pycall/co_fastcall.cpp) with the entry points'
-    addresses and argument classes, or None (then ctypes is used)."""
+    """The fast-call path, or None (then ctypes is used)."""
     global _fast
     if _fast is not None:
         return _fast or None
     _fast = False
     if os.environ.get("CO_NO_FASTCALL") or not os.path.exists(FASTCALL_PATH):
         return None
-    import importlib.machinery
-    import importlib.util
-
-    loader = importlib.machinery.ExtensionFileLoader("_co_fastcall", FASTCALL_PATH)
-    spec = importlib.util.spec_from_file_location("_co_fastcall", FASTCALL_PATH, loader=loader)
-    mod = importlib.util.module_from_spec(spec)
-    loader.exec_module(mod)
-
-    def table(lib, names):
-        return {n: (ctypes.cast(getattr(lib, n), ctypes.c_void_p).value,
-                    "".join(_KIND[t] for t in _SIGS[n]).encode()) for n in names}
-
     try:
-        dev = table(load(), list(_SIGS))
-    except NativeUnavailable:
-        dev = {}
-    host = table(load_host(), HOST_SYMBOLS) if os.path.exists(HOST_LIB_PATH) else {}
-    _fast = (mod.invoke, dev, host)
+        import importlib.machinery
+        import importlib.util
+
+        loader = importlib.machinery.ExtensionFileLoader("_co_fastcall", FASTCALL_PATH)
+        spec = importlib.util.spec_from_file_location("_co_fastcall", FASTCALL_PATH,
+                                                      loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+    except Exception as e:  # built for another interpreter / unloadable: ctypes instead
+        warnings.warn(f"rl4co_slap_amd: fast-call module unusable ({e}); using ctypes",
+                      RuntimeWarning, stacklevel=2)
+        return None
+    _fast = _FastCall(mod.invoke)
     return _fast
 
 
@@ -252,16 +288,11 @@ def call(name, *args):
             raise NotImplementedError(f"{name} has no host (CPU) build; move the TensorDict "
                                       "to the HIP device")
         args = args[:-1] + (None,)
-        if fast:
-            addr, kinds = fast[2][name]
-            rc = fast[0](addr, kinds, *args)
-        else:
-            rc = getattr(lib, name)(*args)
-    elif fast and name in fast[1]:
-        addr, kinds = fast[1][name]
-        rc = fast[0](addr, kinds, *args)
+        ent = fast.table("host").get(name) if fast else None
+        rc = fast.invoke(ent[0], ent[1], *args) if ent else getattr(lib, name)(*args)
     else:
-        rc = getattr(load(), name)(*args)
+        ent = fast.table("dev").get(name) if fast else None
+        rc = fast.invoke(ent[0], ent[1], *args) if ent else getattr(load(), name)(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed with status {rc}")
 
@@ -283,9 +314,53 @@ def bind(name, *args):
     return launch
 
 
-_status_cache = {}
-
-
 def scratch_status(device) -> torch.Tensor:
     """A zeroed device int32 word for data-dependent error bits."""
     return torch.zeros(1, dtype=torch.int32, device=device)
+
+
+# Per-device word that kernels without a caller-held status (gather_by_index) OR their
+# error bits into.  It is read together with the next status read the host makes anyway
+# (an env's reward / status check, post_decoder_hook) -- the analogue of the device-side
+# assert torch.gather raises on a HIP tensor, which also surfaces at the next sync.
+# CO_SYNC_CHECKS=1 reads it right after every such kernel instead (debugging).
+_deferred = {}
+SYNC_CHECKS = bool(os.environ.get("CO_SYNC_CHECKS"))
+_DEFERRED_MSGS = ((ST_INDEX_RANGE, "gather_by_index: index out of range (torch.gather: index "
+                                   "out of bounds for the gathered dimension)"),)
+
+
+def deferred_status(device) -> torch.Tensor:
+    device = torch.device(device)
+    key = (device.type, device.index)
+    w = _deferred.get(key)
+    if w is None:
+        w = _deferred[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return w
+
+
+def pending_deferred(device):
+    """The device's deferred word if one exists (else None): read it with the caller's own
+    status read, then pass the bits to ``raise_deferred``."""
+    device = torch.device(device)
+    return _deferred.get((device.type, device.index))
+
+
+def raise_deferred(bits: int, device) -> None:
+    """Raise the error the deferred bits stand for (clearing the word first, so the error
+    is reported once)."""
+    if not bits:
+        return
+    w = pending_deferred(device) if device is not None else None
+    if w is not None:
+        w.zero_()
+    for bit, msg in _DEFERRED_MSGS:
+        if bits & bit:
+            raise RuntimeError(msg)
+
+
+def check_deferred(device) -> None:
+    """Read (one host sync) and raise the device's deferred error bits."""
+    w = pending_deferred(device)
+    if w is not None:
+        raise_deferred(int(w.item()), device)

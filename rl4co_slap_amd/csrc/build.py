@@ -133,7 +133,18 @@ HOST_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fn
 
 
 FASTCALL_SRC = os.path.join(HERE, "pycall", "co_fastcall.cpp")
-FASTCALL_LIB = os.path.join(OUT_DIR, "_co_fastcall.so")
+
+
+def _ext_suffix() -> str:
+    """The running interpreter's extension suffix (e.g. ``.cpython-310-x86_64-linux-gnu.so``):
+    the fast-call module is built against this interpreter's headers, and the ABI tag in
+    its file name keeps another interpreter from loading it."""
+    import sysconfig
+
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+FASTCALL_LIB = os.path.join(OUT_DIR, "_co_fastcall" + _ext_suffix())
 
 
 def build_fastcall(verbose: bool = False) -> str:

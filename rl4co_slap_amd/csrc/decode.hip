@@ -796,6 +796,206 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Rows longer than the register row engines hold (N > 2048): one 256-thread workgroup
+// per row, the processed logits recomputed from the row in each pass instead of kept in
+// registers.  Always the exact math (ATen's log_softmax bits: SLEEF exp/log, the 16
+// accumulator chains of map_reduce_all walked over 1,024-element LDS chunks by 16
+// threads, the xor-8/4/2/1 butterfly; correctly rounded tanh).  Greedy = first index of
+// the maximal logp (as GreedyRow::select), evaluate, sampling = inverse CDF over the row
+// in index order (statistical parity, like the short rows: a different summation order
+// than DecodeRow's lane layout), top-k by level peeling.  top-p is not offered here.
+namespace {
+
+constexpr int kLongThreads = 256, kLongChunk = 1024;
+
+template <int OPT>
+__device__ __forceinline__ float long_proc(float x, uint8_t mk, float clip, float temp) {
+  float v = x;
+  if (OPT & kOptClip) v = tanh_cr(v) * clip;
+  if (!mk) v = -__builtin_inff();
+  if (OPT & kOptTemp) v = v / temp;  // x / 1 == x: skipped for temp == 1
+  return v;
+}
+
+// block reductions of the 4 waves (every thread returns the result)
+__device__ __forceinline__ float blk_max(float v, float* sh) {
+  v = wave_max(v);
+  if (lane_id() == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ float blk_sum(float v, float* sh) {
+  v = wave_sum(v);
+  if (lane_id() == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ int blk_min_int(int v, int* sh) {
+  v = wave_min_int(v);
+  if (lane_id() == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const int r = min(min(sh[0], sh[1]), min(sh[2], sh[3]));
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ int blk_max_int(int v, int* sh) {
+  return -blk_min_int(-v, sh);
+}
+
+template <int OPT>
+__global__ __launch_bounds__(kLongThreads) void decode_long_kernel(
+    int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
+    const uint8_t* __restrict__ mask, float clip, float temp, int mode,
+    const int64_t* __restrict__ action_in, int64_t* __restrict__ action_out,
+    float* __restrict__ logp_sel, float* __restrict__ full, uint64_t seed, uint64_t offset,
+    int32_t* status, int top_k) {
+  __shared__ float chunk[kLongChunk];
+  __shared__ float shf[4];
+  __shared__ int shi[4];
+  __shared__ float bcast;
+  const float NEG_INF = -__builtin_inff();
+  const int tid = threadIdx.x, lane = lane_id();
+  for (int64_t r = blockIdx.x; r < B; r += gridDim.x) {
+    const float* lrow = logits + r * lstride;
+    const uint8_t* mrow = mask ? mask + r * (int64_t)N : nullptr;
+    auto proc = [&](int c) { return long_proc<OPT>(lrow[c], mrow ? mrow[c] : 1, clip, temp); };
+    float m = NEG_INF;
+    for (int c = tid; c < N; c += kLongThreads) m = fmaxf(m, proc(c));
+    m = blk_max(m, shf);
+    // top-k (decoding.py:112-117): the k-th largest counted with multiplicity
+    float thr = NEG_INF;
+    if (top_k > 0 && top_k < N) {
+      float hi = __builtin_inff();
+      int remaining = top_k;
+      for (int it = 0; it < top_k; ++it) {
+        float lm = NEG_INF;
+        for (int c = tid; c < N; c += kLongThreads) {
+          const float v = proc(c);
+          if (v < hi) lm = fmaxf(lm, v);
+        }
+        lm = blk_max(lm, shf);
+        if (lm == NEG_INF) break;
+        float cnt = 0.f;  // counts < 2^24: exact in f32
+        for (int c = tid; c < N; c += kLongThreads) cnt += proc(c) == lm ? 1.f : 0.f;
+        const int total = (int)blk_sum(cnt, shf);
+        if (total >= remaining) {
+          thr = lm;
+          break;
+        }
+        remaining -= total;
+        hi = lm;
+      }
+    }
+    auto val = [&](int c) {
+      const float v = proc(c);
+      return v < thr ? NEG_INF : v;
+    };
+    // exp-sum in map_reduce_all's order: accumulator j (thread j < 16) adds the
+    // elements c = j (mod 16) left to right, one 1,024-element LDS chunk at a time
+    float acc = 0.f;
+    for (int base = 0; base < N; base += kLongChunk) {
+#pragma unroll
+      for (int q = 0; q < kLongChunk / kLongThreads; ++q) {
+        const int c = base + tid + kLongThreads * q;
+        chunk[tid + kLongThreads * q] = c < N ? aten_expf(val(c) - m) : 0.f;
+      }
+      __syncthreads();
+      if (tid < 16) {
+        const int lim = min(kLongChunk, N - base);
+        for (int i = 0; 16 * i + tid < lim; ++i) {
+          const float e = chunk[16 * i + tid];
+          acc = (base == 0 && i == 0) ? e : acc + e;
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < 64) {  // wave 0: the butterfly of vec_reduce_all on lanes 0..15
+      float v = acc;
+      v += __shfl_xor(v, 8, 16);
+      v += __shfl_xor(v, 4, 16);
+      v += __shfl_xor(v, 2, 16);
+      v += __shfl_xor(v, 1, 16);
+      if (tid == 0) bcast = aten_logf(v);
+    }
+    __syncthreads();
+    const float L = bcast;
+    __syncthreads();
+    auto logp = [&](int c) { return (val(c) - m) - L; };  // ATen association
+    int sel = 0;
+    if (mode == CO_DECODE_GREEDY) {
+      // first index whose logp equals the maximum fl(0 - L) (GreedyRow::select); a NaN L
+      // (all masked / NaN logits) matches nothing: index 0, like torch.argmax over NaNs
+      const float top = 0.f - L;
+      int idx = 0x7fffffff;
+      for (int c = tid; c < N; c += kLongThreads)
+        if (logp(c) == top) {
+          idx = c;
+          break;
+        }
+      idx = blk_min_int(idx, shi);
+      sel = idx == 0x7fffffff ? 0 : idx;
+    } else if (mode == CO_DECODE_SAMPLING) {
+      const uint32_t rr = philox_u32(seed, offset, (uint64_t)r);
+      const float u = (float)(rr >> 8) * (1.0f / 16777216.0f);
+      float own = 0.f;
+      for (int c = tid; c < N; c += kLongThreads) own += expf(logp(c));
+      const float target = u * blk_sum(own, shf);
+      float carry = 0.f;
+      int hit = 0x7fffffff, last = -1;
+      for (int base = 0; base < N; base += kLongThreads) {
+        const int c = base + tid;
+        const float p = c < N ? expf(logp(c)) : 0.f;
+        float incl = p;  // wave inclusive scan, then the earlier waves' totals
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const float t = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += t;
+        }
+        if (lane == 63) shf[tid >> 6] = incl;
+        __syncthreads();
+        float before = carry;
+        for (int w = 0; w < (tid >> 6); ++w) before += shf[w];
+        const float tot = (shf[0] + shf[1]) + (shf[2] + shf[3]);
+        __syncthreads();
+        const float run = before + incl;
+        int h = (p > 0.f && run > target) ? c : 0x7fffffff;
+        h = blk_min_int(h, shi);
+        last = max(last, blk_max_int(p > 0.f ? c : -1, shi));
+        carry += tot;
+        if (h != 0x7fffffff) {
+          hit = h;
+          break;
+        }
+      }
+      sel = hit != 0x7fffffff ? hit : (last >= 0 ? last : 0);
+    } else {
+      const int64_t a = action_in[r];
+      sel = (a < 0 || a >= N) ? 0 : (int)a;
+    }
+    if (full)
+      for (int c = tid; c < N; c += kLongThreads) full[r * (int64_t)N + c] = logp(c);
+    if (tid == 0) {
+      if (mode == CO_DECODE_EVALUATE) {
+        const int64_t a = action_in[r];
+        if (a < 0 || a >= N) set_status(status, CO_ST_INDEX_RANGE);
+        action_out[r] = a;
+      } else {
+        if (mrow && !mrow[sel]) set_status(status, CO_ST_INFEASIBLE);
+        action_out[r] = sel;
+      }
+      if (logp_sel) logp_sel[r] = logp(sel);
+    }
+    __syncthreads();  // the LDS scratch is reused by the next row
+  }
+}
+
+}  // namespace
+
 // RL lanes x EPL consecutive elements per row, by row-length bucket (CO_RL* above).
 #define CO_ROW_DISPATCH(LAUNCH, V)                           \
   if (N <= 16) LAUNCH(CO_RL16, 16 / CO_RL16, V);             \
@@ -874,7 +1074,7 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
                                  double top_p, int mode, const int64_t* action_in,
                                  int64_t* action_out, float* logp_sel, float* full, uint64_t seed,
                                  uint64_t offset, int32_t* status, void* stream) {
-  if (B < 0 || N <= 0 || N > 64 * 32 || top_k < 0 || top_p < 0.0 || top_p > 1.0)
+  if (B < 0 || N <= 0 || N > (1 << 24) || top_k < 0 || top_p < 0.0 || top_p > 1.0)
     return CO_E_INVAL;
   // CO_DECODE_CERTIFIED changes only greedy picks' math (actions stay exact); other modes
   // and the filtered path run the exact math under it
@@ -885,8 +1085,25 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
   if (B == 0) return CO_OK;
   if (!logits || !action_out) return CO_E_INVAL;
   if (mode == CO_DECODE_EVALUATE && !action_in) return CO_E_INVAL;
-  const dim3 grid(decode_grid(B, (int)N)), block(256);
   hipStream_t s = (hipStream_t)stream;
+  if (N > 64 * 32) {  // long rows: workgroup per row, exact math (cert / fast: same actions)
+    if (top_p > 0.0 && top_p < 1.0) return CO_E_INVAL;
+    const dim3 lgrid((unsigned)(B < 65536 ? B : 65536)), lblock(kLongThreads);
+    const int opt = (clip > 0.f ? kOptClip : 0) | (temp != 1.f ? kOptTemp : 0);
+#define CO_LONG(O)                                                                             \
+  hipLaunchKernelGGL(decode_long_kernel<O>, lgrid, lblock, 0, s, B, (int)N, logits, lstride,   \
+                     mask, clip, temp, mode, action_in, action_out, logp_sel, full, seed, offset, \
+                     status, top_k)
+    switch (opt) {
+      case 0: CO_LONG(0); break;
+      case 1: CO_LONG(1); break;
+      case 2: CO_LONG(2); break;
+      default: CO_LONG(3);
+    }
+#undef CO_LONG
+    return launch_status();
+  }
+  const dim3 grid(decode_grid(B, (int)N)), block(256);
   const bool filtered = (top_k > 0 && top_k < N) || (top_p > 0.0 && top_p < 1.0);
   if (mode == CO_DECODE_GREEDY && !filtered) {
 #define CO_GREEDY(RL, EPL, V)                                                                  \

@@ -531,7 +531,8 @@ CO_HOST_API int co_decode_step(int64_t B, int64_t N, const float* logits, int64_
                                const int64_t* action_in, int64_t* action_out, float* logp_sel,
                                float* logp_full, uint64_t seed, uint64_t offset, int32_t* status,
                                void*) {
-  if (mode & CO_DECODE_FAST) mode &= ~CO_DECODE_FAST;  // the host path is always exact
+  // the host path is always exact: the fast / certified math flags select nothing here
+  mode &= ~(CO_DECODE_FAST | CO_DECODE_CERTIFIED);
   if (B < 0 || N <= 0 || mode < 0 || mode > 2) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!logits || !action_out || !logp_sel) return CO_E_INVAL;

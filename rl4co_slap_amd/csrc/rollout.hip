@@ -654,18 +654,51 @@ int launch_tsp_teacher(int64_t B, int64_t N, const float2* l2, int64_t LB, const
 
 }  // namespace
 
+namespace {
+// The episode beyond the fused engines' tiles (teacher N > 256: the coordinate tile no
+// longer fits the LDS; nearest N > 1024: 64 lanes x 16 registers): the same outputs from
+// the stepwise kernels, in place -- co_tsp_reset, then per step [co_tsp_nearest_action
+// +] co_tsp_step (mask / i / first_node updated in place, current_node = the action),
+// then co_tsp_reward on the step-major actions.  N + 2 (2N + 2) launches, no host sync.
+int tsp_rollout_stepwise(int64_t B, int64_t N, const float* locs, const int64_t* acts_in,
+                         int64_t* acts_out, uint8_t* mask_out, int64_t* first_out,
+                         int64_t* cur_out, int64_t* i_out, uint8_t* done_out,
+                         uint8_t* step_reward_out, float* reward_out, int check, int32_t* status,
+                         void* stream) {
+  // reset's reward[B,1] = 0 goes to reward_out, which the episode reward overwrites
+  int rc = co_tsp_reset(B, N, mask_out, first_out, cur_out, i_out, reward_out, stream);
+  const bool nearest = acts_in == nullptr;
+  const int64_t* acts = nearest ? acts_out : acts_in;
+  for (int64_t t = 0; t < N && rc == CO_OK; ++t) {
+    if (nearest)
+      rc = co_tsp_nearest_action(B, N, locs, mask_out, cur_out, t == 0, acts_out + t * B,
+                                 stream);
+    if (rc == CO_OK)
+      rc = co_tsp_step(B, N, acts + t * B, mask_out, mask_out, i_out, i_out, first_out,
+                       first_out, cur_out, done_out, step_reward_out, t == 0 ? 1 : 0, nullptr,
+                       status, stream);
+  }
+  if (rc != CO_OK) return rc;
+  return co_tsp_reward(B, N, N, locs, B, acts, 1, B, check, reward_out, status, stream);
+}
+}  // namespace
+
 extern "C" int co_tsp_rollout(int64_t B, int64_t N, const float* locs, const int64_t* acts_in,
                               int64_t* acts_out, uint8_t* mask_out, int64_t* first_out,
                               int64_t* cur_out, int64_t* i_out, uint8_t* done_out,
                               uint8_t* step_reward_out, float* reward_out, int check,
                               int32_t* status, void* stream) {
-  if (B < 0 || N <= 0 || N > 256) return CO_E_INVAL;
+  if (B < 0 || N <= 0 || N > (1 << 24)) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   const bool nearest = acts_in == nullptr;
   if (!locs || !mask_out || !first_out || !cur_out || !i_out || !done_out || !step_reward_out ||
       !reward_out || (nearest && !acts_out) || (check && !status))
     return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  if (N > (nearest ? 1024 : 256))
+    return tsp_rollout_stepwise(B, N, locs, acts_in, acts_out, mask_out, first_out, cur_out,
+                                i_out, done_out, step_reward_out, reward_out, check, status,
+                                stream);
   if (nearest)  // register-resident lane-group episode (nearest.hip)
     return co_internal_tsp_nearest_rollout(B, N, locs, acts_out, mask_out, first_out, cur_out,
                                            i_out, done_out, step_reward_out, reward_out, stream);

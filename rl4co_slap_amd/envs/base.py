@@ -190,8 +190,15 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
     # -- status word -------------------------------------------------------------
     @staticmethod
     def raise_for_status(status: torch.Tensor, messages):
-        """Read a device status word (one host sync) and raise the reference's error."""
-        bits = int(status.item())
+        """Read a device status word (one host sync, which also carries the device's
+        deferred word: an earlier out-of-range ``gather_by_index``) and raise the
+        reference's error."""
+        d = nat.pending_deferred(status.device) if status.device.type != "cpu" else None
+        if d is not None:
+            bits, dbits = (int(v) for v in torch.cat([status.reshape(1), d]).tolist())
+            nat.raise_deferred(dbits, status.device)
+        else:
+            bits = int(status.item())
         for bit, exc, msg in messages:
             if bits & bit:
                 raise exc(msg)

@@ -7,7 +7,7 @@ import torch
 from torch.distributions import Uniform
 
 from .. import _native as nat
-from ..td import TensorDict
+from ..td import RepeatedRows, TensorDict
 from .base import RL4COEnvBase
 from .common import Generator, device_uniform, get_sampler
 
@@ -120,7 +120,7 @@ class TSPEnv(RL4COEnvBase):
         if not take and first_in is None:
             return None
         b, n = mask.shape
-        if logits.shape != (b, n):
+        if logits.shape != (b, n) or n > 2048:  # long rows: co_decode_step's row kernel
             return None
         dev = mask.device
         mask, i = mask.contiguous(), i.contiguous()
@@ -155,7 +155,7 @@ class TSPEnv(RL4COEnvBase):
         multistart td's un-replicated ``locs`` (``RepeatedRows``) is read in place: env
         ``e`` uses coordinate row ``e % B`` (the kernel's ``locs_batch``)."""
         raw = td.get_raw("locs") if hasattr(td, "get_raw") else td["locs"]
-        locs = getattr(raw, "base", raw)
+        locs = raw.source() if isinstance(raw, RepeatedRows) else raw
         nat.require_device(locs, actions)
         locs = locs.contiguous()
         if actions.dtype != torch.int64:

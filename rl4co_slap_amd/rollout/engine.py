@@ -225,6 +225,12 @@ class SLAPFusedEpisode(_GraphEpisode):
         b, l = locs.shape[0], locs.shape[1]
         p = td["freq"].shape[-2]
         self.b, self.l, self.p, self.policy = b, l, p, policy
+        # co_slap_rollout holds an instance's L locations in 8 registers of up to 32 lanes
+        # (L <= 256); larger warehouses run the same episode as the stepwise launch sequence
+        self._stepwise = SLAPStepwiseEpisode(td, actions, policy) if l > 256 else None
+        if self._stepwise is not None:
+            self.status = self._stepwise.status
+            return
         self.locs = locs.contiguous()
         self.picklist = td["picklist"].contiguous()
         self.o, self.k = self.picklist.shape[1], self.picklist.shape[2]
@@ -253,9 +259,14 @@ class SLAPFusedEpisode(_GraphEpisode):
             nat.ptr(self.status))
 
     def _launch(self, s):
+        if self._stepwise is not None:
+            self._stepwise._launch(s)
+            return
         self._bound(s)
 
     def final_state(self):
+        if self._stepwise is not None:
+            return self._stepwise.final_state()
         return {"action_mask": self.mask, "i": self.i, "assignment": self.assign,
                 "done": self.done, "reward": self.reward, "actions": self.acts.t()}
 
@@ -275,6 +286,12 @@ class CVRPFusedEpisode(_GraphEpisode):
         super().__init__(locs.device)
         d = locs.device
         b, n = locs.shape[0], locs.shape[1]
+        if n > 1023:
+            # the register-resident group engine holds N + 1 <= 1024 nodes (64 lanes x 16);
+            # the stepwise loop (CVRPStepwiseEpisode) has no such limit
+            raise NotImplementedError(
+                f"CVRPFusedEpisode: num_loc={n} > 1023; use CVRPStepwiseEpisode (co_cvrp_rollout "
+                "keeps an instance's nodes in 64 lanes x 16 registers)")
         self.b, self.n, self.vcap = b, n, float(vehicle_capacity)
         self.max_steps = int(max_steps) if max_steps is not None else 2 * n + 1
         self.depot = td["depot"].contiguous()

@@ -28,13 +28,14 @@ import torch
 import torch.distributed as dist
 
 from .. import _native as nat
+from ..utils.decoding import default_decode_math, math_flags
 from .engine import _GraphEpisode
 
 
 class POMOEpisode(_GraphEpisode):
     def __init__(self, locs: torch.Tensor, logits: torch.Tensor, num_starts: int = None,
                  tanh_clipping: float = 10.0, check: bool = True, fast_math: bool = False,
-                 certified: bool = False):
+                 certified: bool = None, decode_math: str = None):
         super().__init__(locs.device)
         b, n, _ = locs.shape
         s = n if num_starts is None else num_starts
@@ -43,9 +44,15 @@ class POMOEpisode(_GraphEpisode):
         d = locs.device
         self.b, self.n, self.s, self.e = b, n, s, e
         self.clip, self.check = float(tanh_clipping), check
-        # fast_math: CO_DECODE_FAST (opt-in; log-probs within ~1e-6, not bit-exact);
-        # certified: CO_DECODE_CERTIFIED (greedy actions = the exact path's, log-probs fast)
-        self.mode = nat.DECODE_FAST if fast_math else (nat.DECODE_CERTIFIED if certified else 0)
+        # decode math (utils/decoding.py _MATH): "certified" by default, as the decoding
+        # strategies (greedy actions = the exact path's, log-probs within 1e-5);
+        # "exact" = ATen bit for bit; "fast" (or fast_math=True) = opt-in approximate.
+        # certified=True / False is the older spelling of "certified" / "exact".
+        if decode_math is None:
+            decode_math = ("fast" if fast_math else "certified" if certified
+                           else "exact" if certified is False else default_decode_math())
+        self.decode_math = decode_math
+        self.mode = math_flags(decode_math)
         self.locs, self.logits = locs.contiguous(), logits.contiguous()
         self.acts = torch.empty((n, e), dtype=torch.int64, device=d)
         self.acts[0] = torch.arange(s, device=d).repeat_interleave(b) % n  # ops.py:150-154
@@ -106,23 +113,38 @@ def shard_range(total: int, world: int, rank: int):
 
 
 def global_metrics(bl: torch.Tensor, max_reward: torch.Tensor, loss_terms: torch.Tensor,
-                   num_starts: int, group=None):
+                   num_starts: int, group=None, total_instances: int = None):
     """All-gather the per-instance shared-baseline results of every rank (RCCL on device
     tensors, gloo on CPU tensors) and form the global POMO metrics: the REINFORCE loss
     ``-(adv * ll).mean()`` over all envs (``reinforce.py:103-105``), the mean reward
-    and the mean multistart max reward (``pomo/model.py:113-114``)."""
+    and the mean multistart max reward (``pomo/model.py:113-114``).
+
+    With ``total_instances`` (the instances over all ranks, sharded by ``shard_range``)
+    every rank knows every shard's size: the exchange is ONE padded all-gather and no host
+    read.  Without it the shard sizes are all-gathered first (a second collective and a
+    host read per rank)."""
     local = torch.stack([bl, max_reward, loss_terms])  # [3, B_local]
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world > 1:
-        sizes = torch.tensor([local.shape[1]], device=local.device)
-        all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-        dist.all_gather(all_sizes, sizes, group=group)
-        mx = int(max(int(x.item()) for x in all_sizes))
+        if total_instances is not None:
+            rank = dist.get_rank(group)
+            sizes = [hi - lo for lo, hi in (shard_range(total_instances, world, r)
+                                            for r in range(world))]
+            if sizes[rank] != local.shape[1]:
+                raise ValueError(f"global_metrics: rank {rank} holds {local.shape[1]} "
+                                 f"instances, shard_range({total_instances}, {world}) gives "
+                                 f"{sizes[rank]}")
+        else:
+            n_local = torch.tensor([local.shape[1]], device=local.device)
+            all_sizes = [torch.zeros_like(n_local) for _ in range(world)]
+            dist.all_gather(all_sizes, n_local, group=group)
+            sizes = [int(x) for x in torch.cat(all_sizes).tolist()]
+        mx = max(sizes)
         pad = torch.zeros((3, mx), dtype=local.dtype, device=local.device)
         pad[:, :local.shape[1]] = local
         bufs = [torch.empty_like(pad) for _ in range(world)]
         dist.all_gather(bufs, pad, group=group)
-        allv = torch.cat([buf[:, :int(n.item())] for buf, n in zip(bufs, all_sizes)], dim=1)
+        allv = torch.cat([buf[:, :n] for buf, n in zip(bufs, sizes)], dim=1)
     else:
         allv = local
     total_inst = allv.shape[1]

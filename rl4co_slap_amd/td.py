@@ -19,10 +19,23 @@ class RepeatedRows:
     (``TensorDict.get_raw``), so an unread ``locs`` is never replicated (655 MB at POMO
     config 5 on one GPU)."""
 
-    __slots__ = ("base", "repeats")
+    __slots__ = ("base", "repeats", "_version")
 
     def __init__(self, base: torch.Tensor, repeats: int):
         self.base, self.repeats = base, repeats
+        # the reference copies at batchify time; the lazy copy is only the same values
+        # while the source is unchanged (an in-place write bumps its version)
+        self._version = base._version
+
+    def source(self) -> torch.Tensor:
+        """``base`` after checking it was not written in place since ``batchify`` (the
+        values the reference's copy holds would be lost: raise instead of reading them)."""
+        if self.base._version != self._version:
+            raise RuntimeError(
+                "batchify: the source tensor was modified in place after batchify; the "
+                "lazy (zero-copy) multistart entry can no longer reproduce the copy the "
+                "reference makes at batchify time. Set CO_EAGER_BATCHIFY=1 to copy eagerly.")
+        return self.base
 
     @property
     def shape(self):
@@ -33,6 +46,7 @@ class RepeatedRows:
         return self.base.device
 
     def materialize(self) -> torch.Tensor:
+        self.source()
         s = self.base.shape
         return self.base.expand(self.repeats, *s).contiguous().view(s[0] * self.repeats, *s[1:])
 

@@ -23,12 +23,40 @@ from .ops import batchify, gather_by_index, unbatchify, unbatchify_and_gather
 _MODES = {"greedy": 0, "sampling": 1, "evaluate": 2}
 _NO_FUSED = bool(__import__("os").environ.get("CO_NO_FUSED_STEP"))  # A/B switch (tests, diag)
 
+# Decode math (the mode word's flag bits, include/co_env.h):
+# * "exact": ATen's CPU log_softmax restated bit for bit (SLEEF expf/logf, map_reduce_all
+#   order, correctly rounded tanh) for every mode;
+# * "certified": greedy picks on the fast math, each row certified by an error bound and
+#   any wave holding an uncertified row recomputed exactly -- the greedy ACTIONS are the
+#   exact path's; the log-probabilities are the fast math's, within 1e-5 (measured ~1e-6)
+#   of the exact ones.  Sampling / evaluate / top-k / top-p / beam ranking stay exact;
+# * "fast": opt-in approximate math everywhere (not bit-exact; benchmarks only).
+# The decoding strategies default to "certified" (CO_DECODE_MATH overrides it); the
+# low-level ``decode_step`` defaults to "exact".
+_MATH = {"exact": 0, "certified": nat.DECODE_CERTIFIED, "fast": nat.DECODE_FAST}
+
+
+def default_decode_math() -> str:
+    m = __import__("os").environ.get("CO_DECODE_MATH", "certified")
+    if m not in _MATH:
+        raise ValueError(f"CO_DECODE_MATH={m!r}: expected one of {sorted(_MATH)}")
+    return m
+
+
+def math_flags(math: str) -> int:
+    try:
+        return _MATH[math]
+    except KeyError:
+        raise ValueError(f"decode_math={math!r}: expected one of {sorted(_MATH)}") from None
+
 
 def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, action=None,
                 return_full=False, seed=None, offset=0, status=None, top_k: int = 0,
-                top_p: float = 0.0):
-    """One fused decode step.  Returns ``(action[B], logp[B], full_logprobs or None)``."""
+                top_p: float = 0.0, math: str = "exact"):
+    """One fused decode step.  Returns ``(action[B], logp[B], full_logprobs or None)``.
+    ``math`` selects the decode math (``_MATH`` above)."""
     nat.require_device(logits, mask, action)
+    flags = math_flags(math)
     if logits.dtype != torch.float32:
         logits = logits.float()
     if logits.stride(-1) != 1:
@@ -48,12 +76,12 @@ def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, act
         assert top_p <= 1.0, "top-p should be in (0, 1]."
         nat.call("co_decode_step_ex", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
                  float(tanh_clipping), float(temperature), min(int(top_k), n), float(top_p),
-                 _MODES[mode], nat.ptr(action), nat.ptr(act_out), nat.ptr(logp), nat.ptr(full),
+                 _MODES[mode] | flags, nat.ptr(action), nat.ptr(act_out), nat.ptr(logp), nat.ptr(full),
                  seed, offset, nat.ptr(status), nat.stream_of(logits))
     else:
         nat.call("co_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
-                 float(tanh_clipping), float(temperature), _MODES[mode], nat.ptr(action),
-                 nat.ptr(act_out), nat.ptr(logp), nat.ptr(full), seed, offset, nat.ptr(status),
+                 float(tanh_clipping), float(temperature), _MODES[mode] | flags,
+                 nat.ptr(action), nat.ptr(act_out), nat.ptr(logp), nat.ptr(full), seed, offset, nat.ptr(status),
                  nat.stream_of(logits))
     return act_out, logp, full
 
@@ -72,7 +100,9 @@ def get_log_likelihood(logprobs, actions=None, mask=None, return_sum: bool = Tru
     """``decoding.py:39-65``.  The ``> -1000`` assert needs a host sync; for logprobs
     that ``post_decoder_hook`` produced, the same test was folded into its single
     status read (``_co_logp_ok``), so no second sync happens here."""
-    checked = getattr(logprobs, "_co_logp_ok", None)
+    rec = getattr(logprobs, "_co_logp_ok", None)
+    # the folded test is valid only while the tensor is unchanged since it was made
+    checked = rec[0] if rec is not None and rec[1] == logprobs._version else None
     if actions is not None and logprobs.dim() == 3:
         logprobs = logprobs.gather(-1, actions.unsqueeze(-1)).squeeze(-1)
     if mask is not None:
@@ -117,8 +147,12 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
                  multisample: bool = False, num_starts: Optional[int] = None,
                  select_start_nodes_fn: Optional[callable] = None,
                  improvement_method_mode: bool = False, select_best: bool = False,
-                 store_all_logp: bool = False, key: str = "action", **kwargs):
+                 store_all_logp: bool = False, key: str = "action",
+                 decode_math: Optional[str] = None, **kwargs):
         self.temperature, self.top_p, self.top_k = temperature, top_p, top_k
+        # "certified" by default: exact greedy actions, log-probabilities within 1e-5
+        self.decode_math = decode_math if decode_math is not None else default_decode_math()
+        self._math_flags = math_flags(self.decode_math)
         self.mask_logits, self.tanh_clipping = mask_logits, tanh_clipping
         self.multistart, self.multisample = multistart, multisample
         self.num_starts, self.select_start_nodes_fn = num_starts, select_start_nodes_fn
@@ -168,11 +202,19 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
                                                                 device=logprobs.device))
         ok = ok.to(torch.int32)
         st = self._status if self._status is not None else torch.zeros_like(ok)
-        st_bits, lp_ok = (int(v) for v in torch.stack([st.reshape(()), ok]).tolist())
+        words = [st.reshape(()), ok]
+        d = nat.pending_deferred(ok.device) if ok.device.type != "cpu" else None
+        if d is not None:  # an out-of-range gather_by_index since the last read
+            words.append(d.reshape(()))
+        vals = [int(v) for v in torch.stack(words).tolist()]
+        st_bits, lp_ok = vals[0], vals[1]
+        if d is not None:
+            nat.raise_deferred(vals[2], ok.device)
         if st_bits & nat.ST_INFEASIBLE:
             raise AssertionError("infeasible action selected")
         if flat:
-            logprobs._co_logp_ok = bool(lp_ok)
+            # the test result holds for these values only: keyed by the tensor's version
+            logprobs._co_logp_ok = (bool(lp_ok), logprobs._version)
         if self.num_starts > 0 and self.select_best:
             logprobs, actions, td, env = self._select_best(logprobs, actions, td, env)
         return logprobs, actions, td, env
@@ -190,7 +232,8 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         sel, logp, full = decode_step(logits, mask, mode, self.temperature, self.tanh_clipping,
                                       action=act_in, return_full=self.store_all_logp,
                                       seed=seed, offset=self._step_idx, status=self._status,
-                                      top_k=self.top_k, top_p=self.top_p)
+                                      top_k=self.top_k, top_p=self.top_p,
+                                      math=self.decode_math)
         self._step_idx += 1
         if mode == "evaluate":
             sel = action
@@ -219,7 +262,7 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         if self._status is None:
             self._status = nat.scratch_status(logits.device)
         seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
-        out = fused(td, logits, _MODES[mode], self.temperature, self.tanh_clipping,
+        out = fused(td, logits, _MODES[mode] | self._math_flags, self.temperature, self.tanh_clipping,
                     action if mode == "evaluate" else None, seed, self._step_idx, self._status,
                     self.key)
         if out is None:
@@ -299,6 +342,10 @@ class BeamSearch(DecodingStrategy):
 
     def __init__(self, beam_width=None, select_best=True, **kwargs):
         kwargs["store_all_logp"] = True
+        # the beams are ranked on the full log-probabilities: only the exact math ranks
+        # them as the reference does (certification covers the argmax alone)
+        if kwargs.get("decode_math") is None:
+            kwargs["decode_math"] = "exact"
         super().__init__(**kwargs)
         self.beam_width = beam_width
         self.select_best = select_best

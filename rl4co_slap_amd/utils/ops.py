@@ -14,6 +14,9 @@ from torch import Tensor
 from .. import _native as nat
 from ..td import TensorDict
 
+# CO_EAGER_BATCHIFY=1: batchify TensorDicts with the reference's eager copy (no lazy rows)
+_EAGER_BATCHIFY = bool(__import__("os").environ.get("CO_EAGER_BATCHIFY"))
+
 
 def _batchify_single(x, repeats: int):
     s = x.shape
@@ -43,7 +46,7 @@ def batchify(x: Union[Tensor, TensorDict], shape):
     for s in reversed(shape):
         if s <= 0:
             continue
-        if hasattr(x, "get_raw") and len(x.batch_size) >= 1:
+        if hasattr(x, "get_raw") and len(x.batch_size) >= 1 and not _EAGER_BATCHIFY:
             x = _batchify_td_lazy(x, s)
         else:
             x = _batchify_single(x, s)
@@ -107,13 +110,20 @@ def gather_by_index(src: Tensor, idx: Tensor, dim: int = 1, squeeze: bool = True
     m = idx2.shape[1]
     es = src.element_size()
     out = torch.empty((*lead, m, *trail), dtype=src.dtype, device=src.device)
-    status = nat.scratch_status(src.device)
+    # out-of-range indices: the device's deferred status word, raised at the next status
+    # read (torch.gather on a HIP tensor raises a device-side assert that likewise
+    # surfaces at the next sync); on the CPU (host build) the check is immediate
+    host = src.device.type == "cpu"
+    status = nat.scratch_status(src.device) if host else nat.deferred_status(src.device)
     nat.call("co_gather_by_index", nat.ptr(flat), outer, flat.shape[1], inner * es,
              flat.stride(0) * es, flat.stride(1) * es, nat.ptr(idx2), m, idx2.stride(0),
              idx2.stride(1), nat.ptr(out), nat.ptr(status), nat.stream_of(src))
+    if host:
+        nat.raise_deferred(int(status.item()), None)
+    elif nat.SYNC_CHECKS:
+        nat.check_deferred(src.device)
     if squeeze and m == 1:
         out = out.squeeze(dim)
-    out._co_status = status  # checked lazily by callers that need the torch error
     return out
 
 

@@ -63,12 +63,15 @@ def test_log_softmax_degenerate_rows():
     assert np.array_equal(got[fin], ref[fin])
 
 
-needs_probe = pytest.mark.skipif(aten_math.probe() is None,
-                                 reason="torch's SLEEF probe needs an AVX512F host")
+def _need_probe():
+    # resolved inside the tests (not at collection): a `-m gpu` run collects this module
+    # and must not map the oracle's probe library
+    if aten_math.probe() is None:
+        pytest.skip("torch's SLEEF probe needs an AVX512F host")
 
 
-@needs_probe
 def test_expf_matches_torch_sleef():
+    _need_probe()
     rng = np.random.default_rng(0)
     # log_softmax feeds exp with x - max <= 0: a dense sweep of the bit patterns of
     # [-104, 0] plus the saturation edges
@@ -80,8 +83,8 @@ def test_expf_matches_torch_sleef():
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
-@needs_probe
 def test_logf_matches_torch_sleef():
+    _need_probe()
     # every f32 in [1, 2) (the mantissa range), then a dense sample of the exp-sum range
     lo = np.arange(0x3F800000, 0x40000000, dtype=np.uint32).view(np.float32)
     rng = np.random.default_rng(1)

@@ -35,7 +35,11 @@ def _worker(rank, world, port, total, starts, q):
     ll = -torch.rand(total, starts, generator=g) * 50
     lo, hi = shard_range(total, world, rank)
     bl, mx, lt = _per_instance(reward[lo:hi], ll[lo:hi])
-    m = global_metrics(bl, mx, lt, starts)
+    # the bench's path: shard sizes from shard_range, one padded all-gather, no host read
+    m = global_metrics(bl, mx, lt, starts, total_instances=total)
+    # sizes exchanged (callers that do not know the total)
+    m2 = global_metrics(bl, mx, lt, starts)
+    assert torch.equal(m["per_instance"], m2["per_instance"])
     if rank == 0:
         q.put({k: (v.item() if torch.is_tensor(v) and v.dim() == 0 else v) for k, v in m.items()
                if k != "per_instance"})
@@ -106,7 +110,7 @@ def _pomo_worker(rank, world, port, n, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard_range(12, world, rank)  # the bench's contiguous balanced shards
     bl, mx, lt = _oracle_pomo_terms(lo, hi, n)
-    m = global_metrics(bl, mx, lt, n)
+    m = global_metrics(bl, mx, lt, n, total_instances=12)
     if rank == 0:
         q.put({k: (v.item() if torch.is_tensor(v) and v.dim() == 0 else v) for k, v in m.items()
                if k != "per_instance"})

@@ -103,8 +103,11 @@ def test_fastcall_path_matches_ctypes_on_the_host_build():
     string for every bound entry point, and gives the ctypes path's results (a host CVRP
     reset: int64, pointer and float arguments, None as the null stream)."""
     fast = _native._fastcall()
-    assert fast is not None, "_co_fastcall.so missing: run the build"
-    invoke, dev, host = fast
+    assert fast is not None, "_co_fastcall module missing: run the build"
+    assert _native.FASTCALL_PATH.endswith(__import__("sysconfig").get_config_var("EXT_SUFFIX"))
+    host = fast.table("host")  # the host table alone: the device library is not needed
+    invoke = fast.invoke
+    dev = fast.table("dev")
     assert set(dev) == set(_native._SIGS)  # every int-returning entry point
     assert set(host) == set(_native.HOST_SYMBOLS)
     assert all(len(k) == len(_native._SIGS[n]) for n, (_, k) in dev.items())
@@ -136,3 +139,16 @@ def test_fastcall_path_matches_ctypes_on_the_host_build():
     addr, kinds = host["co_cvrp_reset"]
     bad = (-1, n) + (0,) * 3 + (1.0,) + (0,) * 7
     assert invoke(addr, kinds, *bad) == lib.co_cvrp_reset(*bad) != 0
+
+
+def test_fastcall_falls_back_to_ctypes_when_a_library_cannot_load(monkeypatch):
+    """A library that fails to load leaves its fast-call table empty: calls then take the
+    ctypes path, which raises the library's own error (no exception from the table)."""
+    fc = _native._FastCall(invoke=None)
+
+    def boom():
+        raise OSError("cannot load")
+
+    monkeypatch.setattr(_native, "load", boom)
+    assert fc.table("dev") == {}
+    assert set(fc.table("host")) == set(_native.HOST_SYMBOLS)

@@ -41,7 +41,7 @@ def main():
     elif a.mode == "pomo":
         out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev)
     elif a.mode == "pomo_cert":
-        out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev, certified=True)
+        out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev, decode_math="certified")
     elif a.mode == "tsp":
         from rl4co_slap_amd.rollout.engine import TSPFusedEpisode
 
