@@ -430,7 +430,8 @@ def main():
     achieved = bytes_per_launch / per_launch / 1e9
     traffic, traffic_src = (None, None)
     if (b, n) == (65536, 100):
-        traffic, traffic_src = pmc_traffic("tsp_fused_teacher", "tsp_teacher_kernel<2, 4, true>")
+        traffic, traffic_src = pmc_traffic("tsp_fused_teacher",
+                                           "tsp_teacher_rows_kernel<16, 8, 2, true>")
 
     out = {
         "metric": "env-steps/sec (batch×decode) SLAP & TSP-100 at 1/2/4/8 MI355X",
@@ -439,10 +440,13 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u8+i64+f32",
         "data": "synthetic: seeded torch.rand TSP instances, teacher-forced argsort actions",
         "config": {"workload": f"TSP-{n} B={b}/GPU teacher-forced episode (reset + {n} env steps + "
-                               "reward + validity) as one fused launch (co_tsp_rollout)",
+                               "reward + validity) as one fused launch (co_tsp_rollout_ex on the "
+                               "reference's row-major [B, N] actions)",
                    "batch_per_gpu": b, "num_loc": n, "env_steps_per_episode": n,
                    "parallelism": f"dp{world}: disjoint instance shards, no data-path collective"},
-        "roofline": {"bound": "hbm", "kernel": "tsp_teacher_kernel<2,4,true> (co_tsp_rollout)",
+        "roofline": {"bound": "hbm",
+                     "kernel": "tsp_teacher_rows_kernel<16,8,2,true> (co_tsp_rollout_ex, "
+                               "row-major [B, N] actions)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      # the same bytes over the wall time `value` uses (launch gaps included)

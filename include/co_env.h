@@ -278,6 +278,19 @@ int co_tsp_rollout(int64_t batch, int64_t num_loc, const float* locs, const int6
                    int64_t* current_node, int64_t* i, uint8_t* done, uint8_t* step_reward,
                    float* reward, int check, int32_t* status, void* stream);
 
+/* co_tsp_rollout with the teacher actions' layout given by strides: element (b, t) at
+ * acts_in[b*act_stride_b + t*act_stride_t].  (1, batch) is co_tsp_rollout's step-major
+ * [N, B]; (>= num_loc, 1) is row-major [B, N] -- the reference's [B, T] layout
+ * (ConstructivePolicy's `actions`, rl4co/models/common/constructive/base.py:223-230): one
+ * lane group per instance reads the instance's contiguous action and coordinate rows
+ * (num_loc <= 1024).  acts_in == NULL: the nearest policy as co_tsp_rollout (strides
+ * unused).  Same outputs as co_tsp_rollout. */
+int co_tsp_rollout_ex(int64_t batch, int64_t num_loc, const float* locs, const int64_t* acts_in,
+                      int64_t act_stride_b, int64_t act_stride_t, int64_t* acts_out,
+                      uint8_t* action_mask, int64_t* first_node, int64_t* current_node,
+                      int64_t* i, uint8_t* done, uint8_t* step_reward, float* reward, int check,
+                      int32_t* status, void* stream);
+
 /* CVRP episode in one launch (cvrp/env.py:73-190 under decoding.py:88-109 rollout):
  * reset from the generator columns (depot[B,2], locs[B,N,2], demand[B,N] already
  * divided by the capacity, vehicle capacity vcap), then the nearest-feasible policy

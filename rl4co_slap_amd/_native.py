@@ -58,6 +58,8 @@ _SIGS = {
     "co_tsp_decode_step": [_i64, _i64, _p, _i64, _p, _f32, _f32, _i32, _p, _p, _p, _u64, _u64, _p,
                            _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p],
     "co_tsp_rollout": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
+    "co_tsp_rollout_ex": [_i64, _i64, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _i32,
+                          _p, _p],
     "co_slap_rollout": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                         _p, _p, _p, _p],
     "co_dihedral8_augment": [_i64, _i64, _p, _p, _p],

@@ -237,6 +237,10 @@ inline int launch_status() {
 int co_internal_tsp_reward_stepmajor(int64_t B, int64_t N, const float* locs,
                                      int64_t locs_batch, const int64_t* acts, int64_t st,
                                      int check, float* reward, int32_t* status, void* stream);
+// internal: rollout.hip's lane-group reward for row-major actions (T == N <= 1024)
+int co_internal_tsp_reward_rows(int64_t B, int64_t N, const float* locs, int64_t locs_batch,
+                                const int64_t* acts, int64_t sb, int check, float* reward,
+                                int32_t* status, void* stream);
 // internal: nearest.hip's register-resident nearest-policy TSP episode
 int co_internal_tsp_nearest_rollout(int64_t B, int64_t N, const float* locs, int64_t* acts_out,
                                     uint8_t* mask_out, int64_t* first_out, int64_t* cur_out,

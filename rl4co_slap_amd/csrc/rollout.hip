@@ -104,7 +104,13 @@ __host__ __device__ inline size_t tsp_tile_bytes(int N, int Q) {
 #ifndef CO_TEACH_U
 #define CO_TEACH_U 8
 #endif
-template <int NW, int Q, bool STATE>
+// NB > 0: a wave's whole step range (<= NB*U steps) is loaded into registers at the
+// kernel's start, in flight together with the coordinate staging, so the walk itself
+// waits on LDS only; NB == 0: U-step batches double-buffered during the walk (long N).
+#ifndef CO_TEACH_NB
+#define CO_TEACH_NB 0
+#endif
+template <int NW, int Q, bool STATE, int NB = 0>
 __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
     int64_t B, int N, const float2* __restrict__ locs, int64_t LB,
     const int64_t* __restrict__ acts_in, uint8_t* __restrict__ mask_out,
@@ -141,7 +147,18 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
   const int nfull = (t_hi - t_lo) / U;
   // wave 0: step 0's action; wave q > 0: the action before its range (previous node)
   const int64_t a_prev = ap[(int64_t)(q == 0 ? 0 : t_lo - 1) * B];
-  if (nfull > 0) load(bufA, t_lo);
+  int64_t pre[NB > 0 ? NB * U : 1];
+  if constexpr (NB > 0) {
+    // every step of the range at once (rows past t_hi re-read the range's last row,
+    // in bounds, never used); the walk below then waits on LDS only
+#pragma unroll
+    for (int j = 0; j < NB * U; ++j) {
+      const int tj = t_lo + j < t_hi ? t_lo + j : (t_hi > 0 ? t_hi - 1 : 0);
+      pre[j] = ap[(int64_t)tj * B];
+    }
+  } else if (nfull > 0) {
+    load(bufA, t_lo);
+  }
   if (q == 0) {
     for (int k = 0; k < NW; ++k) {
       const int lo = k * 64;
@@ -170,19 +187,21 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
     a = in ? (int)lo : 0;
     if (q == 0) {  // step 0 (i == 0 -> first_node = action)
       badw |= in ^ 1u;
-      const uint32_t bit = 1u << (a & 31);
-      const uint32_t old = atomicAnd(&vw[a >> 5], ~bit);
-      badw |= (old & bit) == 0u;
+      // no-return clear: a revisit leaves some node's bit set (N steps, N nodes), which
+      // the final visited words show -- the permutation check of tsp/env.py:168-173
+      __hip_atomic_fetch_and(&vw[a >> 5], ~(1u << (a & 31)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     const float2 p0 = xy[a];
     px = fx = p0.x;
     py = fy = p0.y;
-    // A batch is one basic block: U test-and-clear LDS atomics, U LDS coordinate reads,
-    // U independent edge lengths summed in f32, one f64 add.  Edge lengths use the
-    // hardware v_sqrt_f32 (<= 1 ulp; reward parity is 1e-5 relative).
+    // A batch is one basic block: U LDS coordinate reads, U no-return visited-bit clears
+    // (a revisit shows in the final visited words: N steps over N nodes clear them all
+    // exactly when the actions are a permutation), U independent edge lengths summed in
+    // f32, one f64 add -- one LDS round trip per batch.  Edge lengths use the hardware
+    // v_sqrt_f32 (<= 1 ulp; reward parity is 1e-5 relative).
     auto run = [&](const int64_t (&src)[U], int cnt) {  // cnt: steps used (uniform)
       int av[U];
-      uint32_t old[U], bitv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u < cnt) {
@@ -190,14 +209,20 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
           const uint32_t ok = ((uint32_t)(src[u] >> 32) == 0u) & (l32 < (uint32_t)N);
           badw |= ok ^ 1u;
           av[u] = ok ? (int)l32 : 0;
-          bitv[u] = 1u << (av[u] & 31);
-          old[u] = atomicAnd(&vw[av[u] >> 5], ~bitv[u]);
         }
       }
       float2 qq[U];
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (u < cnt) qq[u] = xy[av[u]];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u < cnt)
+          __hip_atomic_fetch_and(&vw[av[u] >> 5], ~(1u << (av[u] & 31)), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+      // keep the batch's LDS operations issued back to back (the scheduler otherwise
+      // splits the reads into groups with a full wait between them)
+      __builtin_amdgcn_sched_barrier(0);
       float acc = 0.f;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -205,7 +230,6 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
           const float ox = u ? qq[u - 1].x : px, oy = u ? qq[u - 1].y : py;
           const float dx = qq[u].x - ox, dy = qq[u].y - oy;
           acc += __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-          badw |= ((old[u] & bitv[u]) == 0u);  // revisit (tsp/env.py:168-173)
         }
       }
       len += (double)acc;
@@ -217,26 +241,40 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
           a = av[u];
         }
     };
-    int k = 0;
-    for (; k + 1 < nfull; k += 2) {
-      load(bufB, t_lo + (k + 1) * U);
-      run(bufA, U);
-      load(bufA, t_lo + (k + 2) * U);
-      run(bufB, U);
-    }
-    if (k < nfull) run(bufA, U);
-    const int tail = t_hi - t_lo - nfull * U;  // < U steps left
-    if (tail > 0) {
-      const int t0 = t_lo + nfull * U;
+    if constexpr (NB > 0) {
+      const int cnt = t_hi - t_lo;
 #pragma unroll
-      for (int u = 0; u < U; ++u) bufB[u] = (u < tail) ? ap[(int64_t)(t0 + u) * B] : 0;
-      run(bufB, tail);
+      for (int kb = 0; kb < NB; ++kb) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) bufA[u] = pre[kb * U + u];
+        if (cnt >= (kb + 1) * U)
+          run(bufA, U);  // full batch: straight-line code (a compile-time count)
+        else if (cnt > kb * U)
+          run(bufA, cnt - kb * U);
+      }
+    } else {
+      int k = 0;
+      for (; k + 1 < nfull; k += 2) {
+        load(bufB, t_lo + (k + 1) * U);
+        run(bufA, U);
+        load(bufA, t_lo + (k + 2) * U);
+        run(bufB, U);
+      }
+      if (k < nfull) run(bufA, U);
+      const int tail = t_hi - t_lo - nfull * U;  // < U steps left
+      if (tail > 0) {
+        const int t0 = t_lo + nfull * U;
+#pragma unroll
+        for (int u = 0; u < U; ++u) bufB[u] = (u < tail) ? ap[(int64_t)(t0 + u) * B] : 0;
+        run(bufB, tail);
+      }
     }
   }
 #if defined(CO_DIAG_PHASE) && CO_DIAG_PHASE == 2
   if (live && q == 0) reward_out[b] = -(float)len + (float)(vw[0] & 1) + (badw ? 1.f : 0.f);
   return;
 #endif
+  // out-of-range actions seen by this wave (revisits: from the final words below)
   if (__any(badw != 0u && check) && lane == 0) set_status(status, CO_ST_INVALID_TOUR);
   __syncthreads();  // steps done: the coordinate tile is free, the visited words final
   // scratch in the tile region: [64][N] mask bytes, then per-wave partial sums and the
@@ -257,6 +295,10 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
   bool empty = true;
 #pragma unroll
   for (int kk = 0; kk < NW; ++kk) empty &= (m[kk] == 0);
+  // a node left unvisited after N steps = some node visited twice (or an out-of-range
+  // action, already flagged): not a permutation
+  if (q == 0 && __any(live && !empty && check) && lane == 0)
+    set_status(status, CO_ST_INVALID_TOUR);
   // Every instance of the tile fully visited (any valid tour): its mask rows are all zero
   // and are stored as zeros, without the LDS expansion and its read-back.
   int* s_flag = s_lasta + 64;  // [Q]
@@ -301,6 +343,206 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
       zero_tile_out(rows * N, mask_out + row0 * N);
     else
       copy_tile_out(smem, rows * N, mask_out + row0 * N);
+  }
+}
+
+// Teacher-forced TSP episode on ROW-MAJOR actions [B, N] (element (b, t) at
+// acts[b*sb + t]: the reference's own [B, T] layout, ConstructivePolicy's `actions`):
+// G lanes per instance, lane sl owns the EPL consecutive steps t = sl*EPL + k.  Every
+// input is read as a contiguous row -- the instance's 8N bytes of actions in 16-byte
+// vectors, its 8N bytes of coordinates gathered within one row (whole lines, L2) -- and
+// nothing is staged in LDS, so all of B is in flight without tile rounds.  The visited set
+// is a per-group LDS bitmap (no-return ds_or per step); the actions are a permutation iff
+// all N bits are set after the N steps (and every action is in range).  Edge lengths in
+// f32 (hardware sqrt, <= 1 ulp; reward parity is 1e-5 relative): within a lane, to the
+// next lane's first step (lane shuffle) and the closing edge, lane sums added in f64.
+// STATE = false: reward + validity only (co_tsp_reward on row-major actions, T == N);
+// coordinates of env e come from row e % LB (POMO multistart).
+#ifndef CO_ROWS_DMA
+#define CO_ROWS_DMA 1  // the row kernel stages a wave's rows by LDS-DMA when it can
+#endif
+// LDS bytes per wave of the LDS-DMA variant: the wave's GPW coordinate rows and action
+// rows, contiguous in memory, land in LDS as two blocks of GPW*N*8 bytes.
+__host__ __device__ inline size_t tsp_rows_wave_bytes(int gpw, int N) {
+  return (((size_t)gpw * N * 8 + 15) & ~(size_t)15) * 2;
+}
+
+// The wave copies `nbytes` (16-byte aligned source and destination) global -> LDS with
+// LDS-DMA, 1 KiB per instruction; the caller waits (vmcnt) before reading.
+__device__ __forceinline__ void wave_dma(const unsigned char* __restrict__ src, int nbytes,
+                                         unsigned char* dst) {
+  const int lane = lane_id(), n16 = nbytes & ~15;
+  for (int base = 0; base < n16; base += 1024) {
+    if (base + lane * 16 < n16)
+      __builtin_amdgcn_global_load_lds((const void*)(src + base + lane * 16),
+                                       (lds_void*)(dst + base), 16, 0, 0);
+  }
+  if (lane < ((nbytes - n16) >> 2))  // an 8-byte tail (odd N): plain loads
+    reinterpret_cast<uint32_t*>(dst + n16)[lane] = reinterpret_cast<const uint32_t*>(src + n16)[lane];
+}
+
+// MODE 0: scalar 8-byte action loads; 1: 16-byte vectors (16-byte aligned rows); 2: the
+// wave's GPW action and coordinate rows (contiguous: sb == N, consecutive coordinate
+// rows) staged by LDS-DMA as two contiguous blocks, steps and gathers then read from LDS.
+template <int G, int EPL, int MODE, bool STATE>
+__global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
+    int64_t B, int N, const float2* __restrict__ locs, int64_t LB,
+    const int64_t* __restrict__ acts, int64_t sb, uint8_t* __restrict__ mask_out,
+    int64_t* __restrict__ first_out, int64_t* __restrict__ cur_out, int64_t* __restrict__ i_out,
+    uint8_t* __restrict__ done_out, uint8_t* __restrict__ step_reward_out,
+    float* __restrict__ reward_out, int check, int32_t* status) {
+  constexpr int GPW = 64 / G;
+  constexpr bool VEC = MODE == 1, DMA = MODE == 2;
+  __shared__ uint32_t s_bits[4][GPW][(G * EPL + 31) / 32];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_rows[];  // DMA: per wave
+  constexpr int NWB = (G * EPL + 31) / 32;
+  const int lane = lane_id(), sl = lane % G, grp = lane / G, w = threadIdx.x >> 6;
+  uint32_t* bits = s_bits[w][grp];
+  const size_t half = DMA ? tsp_rows_wave_bytes(GPW, N) / 2 : 0;
+  unsigned char* s_w = s_rows + (DMA ? (size_t)w * 2 * half : 0);
+  const float2* s_xy = reinterpret_cast<const float2*>(s_w);
+  const int64_t* s_act = reinterpret_cast<const int64_t*>(s_w + half);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
+  const int nwords = (N + 31) >> 5;
+  const int t0 = sl * EPL;
+  for (int64_t base = wid * GPW; base < B; base += nwaves * GPW) {
+    const int64_t r = base + grp;
+    const bool valid = r < B;
+    const int64_t rr = valid ? r : 0;
+    const int64_t* arow = acts + rr * sb;
+    if constexpr (DMA) {
+      // the previous rows' LDS reads are done before the DMA overwrites them
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      const int rows = (int)(B - base < GPW ? B - base : GPW);
+      const int64_t lb = LB == B ? base : base % LB;
+      wave_dma(reinterpret_cast<const unsigned char*>(locs + lb * N), rows * N * 8, s_w);
+      wave_dma(reinterpret_cast<const unsigned char*>(acts + base * (int64_t)N), rows * N * 8,
+               s_w + half);
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // the lane's EPL actions: 16-byte vectors when the row is 16-byte aligned
+    int64_t av[EPL];
+    if constexpr (DMA) {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) av[k] = (valid && t0 + k < N) ? s_act[grp * N + t0 + k] : 0;
+    } else if constexpr (VEC) {
+#pragma unroll
+      for (int k = 0; k < EPL; k += 2) {
+        if (valid && t0 + k + 1 < N) {
+          const longlong2 v = *reinterpret_cast<const longlong2*>(arow + t0 + k);
+          av[k] = v.x;
+          av[k + 1] = v.y;
+        } else {
+          av[k] = (valid && t0 + k < N) ? arow[t0 + k] : 0;
+          av[k + 1] = 0;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) av[k] = (valid && t0 + k < N) ? arow[t0 + k] : 0;
+    }
+    for (int j = sl; j < NWB; j += G) bits[j] = 0u;
+    uint32_t bad = 0;
+    int node[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      const uint32_t l32 = (uint32_t)av[k];
+      const bool ok = ((uint32_t)(av[k] >> 32) == 0u) & (l32 < (uint32_t)N);
+      const bool in = t0 + k < N;
+      bad |= (in && !ok) ? 1u : 0u;
+      node[k] = ok ? (int)l32 : 0;
+    }
+    const float2* lrow = DMA ? s_xy + grp * N : locs + (LB == B ? rr : rr % LB) * (int64_t)N;
+    float2 p[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) p[k] = (valid && t0 + k < N) ? lrow[node[k]] : make_float2(0.f, 0.f);
+    // the zeroed bitmap is visible to the group's other lanes (one wave, in order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < EPL; ++k)
+      if (valid && t0 + k < N)
+        __hip_atomic_fetch_or(&bits[node[k] >> 5], 1u << (node[k] & 31), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+    // edges: within the lane, to the next lane's first step, and the closing edge
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 1; k < EPL; ++k)
+      if (t0 + k < N) {
+        const float dx = p[k].x - p[k - 1].x, dy = p[k].y - p[k - 1].y;
+        acc += __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+      }
+    const float nx = __shfl_down(p[0].x, 1, G), ny = __shfl_down(p[0].y, 1, G);
+    const float fx = __shfl(p[0].x, 0, G), fy = __shfl(p[0].y, 0, G);  // step 0
+    const int tl = N - 1 - t0;  // this lane's slot of step N-1 (if 0 <= tl < EPL)
+    float lx = p[EPL - 1].x, ly = p[EPL - 1].y;
+#pragma unroll
+    for (int k = 0; k < EPL - 1; ++k)
+      if (k == tl) {
+        lx = p[k].x;
+        ly = p[k].y;
+      }
+    if (t0 + EPL < N) {  // edge (t0 + EPL - 1) -> (t0 + EPL), the next lane's first step
+      const float dx = nx - lx, dy = ny - ly;
+      acc += __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+    } else if (tl >= 0 && tl < EPL) {  // closing edge: step N-1 -> step 0 (roll by -1)
+      acc += edge_len(lx, ly, fx, fy);
+    }
+    double len = (double)acc;
+#pragma unroll
+    for (int d = G / 2; d >= 1; d >>= 1) len += __shfl_xor(len, d, G);
+    // visited words: all N bits set <=> the N actions are a permutation (given in range)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int cnt = 0;
+    for (int j = sl; j < nwords; j += G) cnt += __popc(bits[j]);
+    cnt = (int)grp_reduce<G>((uint32_t)cnt, [](uint32_t x, uint32_t y) { return x + y; });
+    bad = grp_reduce<G>(bad, [](uint32_t x, uint32_t y) { return x | y; });
+    const bool full = cnt == N;
+    if (check && valid && sl == 0 && (bad || !full)) set_status(status, CO_ST_INVALID_TOUR);
+    if (!valid) continue;
+    if constexpr (STATE) {
+      // action_mask row: byte c = node c not visited (all zero for a permutation)
+      uint8_t* mrow = mask_out + r * (int64_t)N;
+      const bool wide = ((reinterpret_cast<uintptr_t>(mrow) | (uintptr_t)N) & 3) == 0;
+      if (wide) {
+        for (int c4 = sl; c4 < (N >> 2); c4 += G) {
+          uint32_t v = 0;
+          if (!full) {
+            const uint32_t nib = ~(bits[c4 >> 3] >> (4 * (c4 & 7))) & 0xfu;
+            v = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
+          }
+          *reinterpret_cast<uint32_t*>(mrow + 4 * c4) = v;
+        }
+      } else {
+        for (int c = sl; c < N; c += G)
+          mrow[c] = full ? 0 : (uint8_t)(((bits[c >> 5] >> (c & 31)) & 1u) ^ 1u);
+      }
+      // row scalars spread over the group's lanes
+      const int last_lane = (N - 1) / EPL;
+      int lastnode = node[0];
+#pragma unroll
+      for (int k = 0; k < EPL; ++k)
+        if (k == tl) lastnode = node[k];
+      if (sl == 0) {
+        first_out[r] = node[0];
+        i_out[r] = N;
+        reward_out[r] = -(float)len;
+      }
+      if (sl == last_lane) cur_out[r] = lastnode;
+      if (sl == (G > 2 ? 2 : 1) % G) {
+        done_out[r] = full;
+        step_reward_out[r] = 0;
+      }
+    } else {
+      if (sl == 0) reward_out[r] = -(float)len;
+    }
   }
 }
 
@@ -632,27 +874,83 @@ int launch_tsp_teacher(int64_t B, int64_t N, const float2* l2, int64_t LB, const
                        uint8_t* mask_out, int64_t* first_out, int64_t* cur_out, int64_t* i_out,
                        uint8_t* done_out, uint8_t* step_reward_out, float* reward_out, int check,
                        int32_t* status, hipStream_t s) {
-  constexpr int Q = CO_TEACH_Q;
+  constexpr int Q = CO_TEACH_Q, PRE = CO_TEACH_NB;
   const int NW = NW_launch(N);
   const size_t shmem = tsp_tile_bytes((int)N, Q) + (size_t)64 * (2 * NW + 1) * 4;
   const dim3 grid((unsigned)((B + 63) / 64)), block(64 * Q);
-#define CO_TEACH(W)                                                                            \
+  // a wave's step range fits the register prefetch: R = ceil((N - 1) / Q) <= PRE * U
+  const bool pre = PRE > 0 && (N - 1 + Q - 1) / Q <= PRE * CO_TEACH_U;
+#define CO_TEACH(W, P)                                                                         \
   do {                                                                                         \
     if (shmem > 64 * 1024)                                                                     \
-      (void)hipFuncSetAttribute((const void*)tsp_teacher_kernel<W, Q, STATE>,                  \
+      (void)hipFuncSetAttribute((const void*)tsp_teacher_kernel<W, Q, STATE, P>,               \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);       \
-    hipLaunchKernelGGL((tsp_teacher_kernel<W, Q, STATE>), grid, block, shmem, s, B, (int)N,    \
+    hipLaunchKernelGGL((tsp_teacher_kernel<W, Q, STATE, P>), grid, block, shmem, s, B, (int)N, \
                        l2, LB, acts, mask_out, first_out, cur_out, i_out, done_out,                \
                        step_reward_out, reward_out, check, status);                            \
   } while (0)
-  if (NW == 1) CO_TEACH(1);
-  else if (NW == 2) CO_TEACH(2);
-  else CO_TEACH(4);
+  if (NW == 1) {
+    if (pre) CO_TEACH(1, PRE);
+    else CO_TEACH(1, 0);
+  } else if (NW == 2) {
+    if (pre) CO_TEACH(2, PRE);
+    else CO_TEACH(2, 0);
+  } else {
+    CO_TEACH(4, 0);
+  }
 #undef CO_TEACH
   return launch_status();
 }
 
+template <bool STATE>
+int launch_tsp_rows(int64_t B, int64_t N, const float2* l2, int64_t LB, const int64_t* acts,
+                    int64_t sb, uint8_t* mask_out, int64_t* first_out, int64_t* cur_out,
+                    int64_t* i_out, uint8_t* done_out, uint8_t* step_reward_out,
+                    float* reward_out, int check, int32_t* status, hipStream_t s) {
+  const bool vec = ((reinterpret_cast<uintptr_t>(acts) & 15) == 0) && (sb % 2 == 0);
+  // LDS-DMA staging: contiguous rows (sb == N), 16-byte aligned blocks (the wave's GPW rows
+  // start at a multiple of 32N bytes), the multistart row map not wrapping inside a wave
+  const bool dma_ok = CO_ROWS_DMA && sb == N &&
+                      ((reinterpret_cast<uintptr_t>(acts) | reinterpret_cast<uintptr_t>(l2)) & 15) == 0;
+#define CO_ROWS(GG, EE)                                                                        \
+  do {                                                                                         \
+    const dim3 grid(grid_for((B + 64 / GG - 1) / (64 / GG), 4, 256 * 32)), block(256);        \
+    const size_t dsh = 4 * tsp_rows_wave_bytes(64 / GG, (int)N);                               \
+    if (dma_ok && (LB == B || LB % (64 / GG) == 0) && dsh <= 64 * 1024)                        \
+      hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 2, STATE>), grid, block, dsh, s, B,   \
+                         (int)N, l2, LB, acts, sb, mask_out, first_out, cur_out, i_out,        \
+                         done_out, step_reward_out, reward_out, check, status);                \
+    else if (vec)                                                                              \
+      hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 1, STATE>), grid, block, 0, s, B,     \
+                         (int)N, l2, LB, acts, sb, mask_out, first_out, cur_out, i_out,        \
+                         done_out, step_reward_out, reward_out, check, status);                \
+    else                                                                                       \
+      hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 0, STATE>), grid, block, 0, s, B,     \
+                         (int)N, l2, LB, acts, sb, mask_out, first_out, cur_out, i_out,        \
+                         done_out, step_reward_out, reward_out, check, status);                \
+  } while (0)
+  if (N <= 32) CO_ROWS(4, 8);
+  else if (N <= 64) CO_ROWS(8, 8);
+  else if (N <= 128) CO_ROWS(16, 8);
+  else if (N <= 256) CO_ROWS(32, 8);
+  else if (N <= 512) CO_ROWS(64, 8);
+  else CO_ROWS(64, 16);
+#undef CO_ROWS
+  return launch_status();
+}
+
 }  // namespace
+
+// Reward + permutation check for row-major actions (element (b, t) at acts[b*sb + t]),
+// T == N <= 1024: the row kernel without the state outputs.  Called by co_tsp_reward.
+int co_internal_tsp_reward_rows(int64_t B, int64_t N, const float* locs, int64_t locs_batch,
+                                const int64_t* acts, int64_t sb, int check, float* reward,
+                                int32_t* status, void* stream) {
+  if (N > 1024 || sb < N || (reinterpret_cast<uintptr_t>(locs) & 7)) return CO_E_INVAL;
+  return launch_tsp_rows<false>(B, N, reinterpret_cast<const float2*>(locs), locs_batch, acts, sb,
+                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, reward,
+                                check, status, (hipStream_t)stream);
+}
 
 namespace {
 // The episode beyond the fused engines' tiles (teacher N > 256: the coordinate tile no
@@ -683,11 +981,12 @@ int tsp_rollout_stepwise(int64_t B, int64_t N, const float* locs, const int64_t*
 }
 }  // namespace
 
-extern "C" int co_tsp_rollout(int64_t B, int64_t N, const float* locs, const int64_t* acts_in,
-                              int64_t* acts_out, uint8_t* mask_out, int64_t* first_out,
-                              int64_t* cur_out, int64_t* i_out, uint8_t* done_out,
-                              uint8_t* step_reward_out, float* reward_out, int check,
-                              int32_t* status, void* stream) {
+extern "C" int co_tsp_rollout_ex(int64_t B, int64_t N, const float* locs,
+                                 const int64_t* acts_in, int64_t sb, int64_t st,
+                                 int64_t* acts_out, uint8_t* mask_out, int64_t* first_out,
+                                 int64_t* cur_out, int64_t* i_out, uint8_t* done_out,
+                                 uint8_t* step_reward_out, float* reward_out, int check,
+                                 int32_t* status, void* stream) {
   if (B < 0 || N <= 0 || N > (1 << 24)) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   const bool nearest = acts_in == nullptr;
@@ -695,6 +994,13 @@ extern "C" int co_tsp_rollout(int64_t B, int64_t N, const float* locs, const int
       !reward_out || (nearest && !acts_out) || (check && !status))
     return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  if (!nearest && !(sb == 1 && st == B)) {
+    // row-major teacher actions (the reference's [B, T]): one lane group per instance
+    if (st != 1 || sb < N || N > 1024) return CO_E_INVAL;
+    return launch_tsp_rows<true>(B, N, reinterpret_cast<const float2*>(locs), B, acts_in, sb,
+                                 mask_out, first_out, cur_out, i_out, done_out, step_reward_out,
+                                 reward_out, check, status, (hipStream_t)stream);
+  }
   if (N > (nearest ? 1024 : 256))
     return tsp_rollout_stepwise(B, N, locs, acts_in, acts_out, mask_out, first_out, cur_out,
                                 i_out, done_out, step_reward_out, reward_out, check, status,
@@ -707,6 +1013,15 @@ extern "C" int co_tsp_rollout(int64_t B, int64_t N, const float* locs, const int
                                   mask_out,
                                   first_out, cur_out, i_out, done_out, step_reward_out,
                                   reward_out, check, status, (hipStream_t)stream);
+}
+
+extern "C" int co_tsp_rollout(int64_t B, int64_t N, const float* locs, const int64_t* acts_in,
+                              int64_t* acts_out, uint8_t* mask_out, int64_t* first_out,
+                              int64_t* cur_out, int64_t* i_out, uint8_t* done_out,
+                              uint8_t* step_reward_out, float* reward_out, int check,
+                              int32_t* status, void* stream) {
+  return co_tsp_rollout_ex(B, N, locs, acts_in, 1, B, acts_out, mask_out, first_out, cur_out,
+                           i_out, done_out, step_reward_out, reward_out, check, status, stream);
 }
 
 // Reward + permutation check for step-major actions (element (b, t) at acts[t*st + b]),

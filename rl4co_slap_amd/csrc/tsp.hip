@@ -310,6 +310,12 @@ extern "C" int co_tsp_reward(int64_t B, int64_t N, int64_t T, const float* locs,
       (locs_batch == B || locs_batch % 64 == 0) && (reinterpret_cast<uintptr_t>(locs) & 15) == 0)
     return co_internal_tsp_reward_stepmajor(B, N, locs, locs_batch, actions, st, check, reward,
                                             status, stream);
+  // row-major actions ([B, T], the reference's layout), T == N: lane group per instance,
+  // contiguous rows (rollout.hip)
+  if (st == 1 && sb >= T && T == N && N <= 1024 &&
+      (locs_batch == B || B % locs_batch == 0))
+    return co_internal_tsp_reward_rows(B, N, locs, locs_batch, actions, sb, check, reward,
+                                       status, stream);
   const size_t words = (size_t)((T + 31) / 32);
   constexpr int W = 4;
   const size_t shmem = check ? W * words * sizeof(uint32_t) : 0;

@@ -171,20 +171,26 @@ class SLAPStepwiseEpisode(_GraphEpisode):
 
 
 class TSPFusedEpisode(_GraphEpisode):
-    """The whole TSP episode as ONE launch (``co_tsp_rollout``): reset, N steps with the
-    policy in-kernel (teacher-forced step-major actions, or nearest-unvisited) and the
-    reward, state in registers/LDS; writes the post-rollout TensorDict columns."""
+    """The whole TSP episode as ONE launch (``co_tsp_rollout_ex``): reset, N steps with the
+    policy in-kernel (teacher-forced actions, or nearest-unvisited) and the reward, state
+    in registers/LDS; writes the post-rollout TensorDict columns.
+
+    Teacher actions stay in the caller's row-major ``[B, N]`` layout (the reference's
+    ``[B, T]``: one lane group per instance reads contiguous rows) for N <= 1024;
+    ``layout="steps"`` (or N > 1024) transposes them once to the step-major ``[N, B]`` the
+    stepwise kernels read (the LDS-tile engine)."""
 
     def __init__(self, locs: torch.Tensor, actions: torch.Tensor = None, policy: str = "teacher",
-                 check: bool = True):
+                 check: bool = True, layout: str = "rows"):
         super().__init__(locs.device)
         b, n, _ = locs.shape
         d = locs.device
         self.b, self.n, self.policy, self.check = b, n, policy, check
         self.locs = locs.contiguous()
+        self.rows = policy == "teacher" and layout == "rows" and n <= 1024
         if policy == "teacher":
             assert actions is not None and actions.shape == (b, n)
-            self.acts = actions.t().contiguous()
+            self.acts = actions.long().contiguous() if self.rows else actions.t().contiguous()
         else:
             self.acts = torch.empty((n, b), dtype=torch.int64, device=d)
         self.mask = torch.empty((b, n), dtype=torch.bool, device=d)
@@ -197,9 +203,11 @@ class TSPFusedEpisode(_GraphEpisode):
         self.status = torch.zeros(1, dtype=torch.int32, device=d)
 
         teacher = self.policy == "teacher"
+        sb, st = (n, 1) if self.rows else (1, b)
         self._bound = nat.bind(
-            "co_tsp_rollout", self.b, self.n, nat.ptr(self.locs),
-            nat.ptr(self.acts) if teacher else None, None if teacher else nat.ptr(self.acts),
+            "co_tsp_rollout_ex", self.b, self.n, nat.ptr(self.locs),
+            nat.ptr(self.acts) if teacher else None, sb, st,
+            None if teacher else nat.ptr(self.acts),
             nat.ptr(self.mask), nat.ptr(self.first), nat.ptr(self.cur), nat.ptr(self.i),
             nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.reward),
             int(self.check), nat.ptr(self.status))
@@ -210,7 +218,7 @@ class TSPFusedEpisode(_GraphEpisode):
     def final_state(self):
         return {"action_mask": self.mask, "i": self.i, "first_node": self.first,
                 "current_node": self.cur, "done": self.done, "reward": self.reward,
-                "actions": self.acts.t()}
+                "actions": self.acts if self.rows else self.acts.t()}
 
 
 class SLAPFusedEpisode(_GraphEpisode):

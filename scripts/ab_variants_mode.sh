@@ -7,7 +7,9 @@ if [ -n "$TESTS" ]; then
 fi
 for r in 1 2 3; do
   for v in ${VARIANTS:-base}; do
-    if [ $v = base ]; then L=rl4co_slap_amd/_lib/libco_env.so; else L=tools/_variants/libco_env_$v.so; fi
-    echo "$v $(CO_LIB=$L timeout -k 10 120 python tools/run_mode.py ${MODE:-tsp} --k ${K:-5} 2>/dev/null | tail -1 | cut -c1-400)" || exit 1
+    # a variant "NAME@steps" runs NAME with the step-major TSP layout (CO_TSP_LAYOUT)
+    lay=rows; vv=$v; case $v in *@*) lay=${v#*@}; vv=${v%@*};; esac
+    if [ $vv = base ]; then L=rl4co_slap_amd/_lib/libco_env.so; else L=tools/_variants/libco_env_$vv.so; fi
+    echo "$v $(CO_TSP_LAYOUT=$lay CO_LIB=$L timeout -k 10 120 python tools/run_mode.py ${MODE:-tsp} --k ${K:-5} 2>/dev/null | tail -1 | cut -c1-400)" || exit 1
   done
 done

@@ -5,9 +5,17 @@ import torch
 
 from oracle.envs import TSPOracle, tsp_nearest_action
 from oracle.rollout import rollout as ref_rollout
+import functools
+
 from rl4co_slap_amd.rollout.engine import TSPFusedEpisode, TSPStepwiseEpisode
 
 pytestmark = pytest.mark.gpu
+
+# the fused episode on both action layouts: row-major [B, N] (lane group per instance,
+# the default) and step-major [N, B] (the LDS-tile engine)
+ROWS = functools.partial(TSPFusedEpisode, layout="rows")
+STEPS = functools.partial(TSPFusedEpisode, layout="steps")
+LAYOUTS = pytest.mark.parametrize("fused", [ROWS, STEPS], ids=["rows", "steps"])
 
 
 def _ref(b, n, seed, policy):
@@ -34,7 +42,7 @@ def _check(state, a, r, tdf, exact_reward=False):
     assert ((got - r).abs() <= 1e-5 * r.abs().clamp(min=1)).all()
 
 
-@pytest.mark.parametrize("cls", [TSPFusedEpisode, TSPStepwiseEpisode])
+@pytest.mark.parametrize("cls", [ROWS, STEPS, TSPStepwiseEpisode], ids=["rows", "steps", "stepwise"])
 @pytest.mark.parametrize("b,n", [(1, 5), (100, 20), (256, 100), (77, 64), (65, 65), (40, 150)])
 @pytest.mark.parametrize("policy", ["teacher", "nearest"])
 def test_tsp_rollout_matches_oracle(dev, cls, b, n, policy):
@@ -51,24 +59,26 @@ def test_tsp_rollout_matches_oracle(dev, cls, b, n, policy):
     _check(ep.final_state(), a, r, tdf)
 
 
-def test_tsp_fused_invalid_tour_flag(dev):
+@LAYOUTS
+def test_tsp_fused_invalid_tour_flag(dev, fused):
     b, n = 70, 12
     locs = torch.rand(b, n, 2)
     acts = torch.arange(n).repeat(b, 1)
     acts[33, 5] = 7  # duplicate -> not a permutation
-    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep = fused(locs.to(dev), acts.to(dev))
     ep.run_eager()
     torch.cuda.synchronize()
     assert int(ep.status.item()) & 1
 
 
-def test_tsp_fused_full_size_properties(dev):
+@LAYOUTS
+def test_tsp_fused_full_size_properties(dev, fused):
     # BASELINE config 2 size: size-independent properties (oracle too slow to mirror whole)
     b, n = 65536, 100
     g = torch.Generator().manual_seed(1234)
     locs = torch.rand(b, n, 2, generator=g)
     acts = torch.rand(b, n, generator=torch.Generator().manual_seed(4321)).argsort(1)
-    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep = fused(locs.to(dev), acts.to(dev))
     ep.run_eager()
     torch.cuda.synchronize()
     st = ep.final_state()
@@ -84,21 +94,22 @@ def test_tsp_fused_full_size_properties(dev):
     got = st["reward"].cpu()
     assert ((got - ref).abs() <= 1e-5 * ref.abs().clamp(min=1)).all()
     # rotation invariance of the closed tour length
-    ep2 = TSPFusedEpisode(locs.to(dev), acts.roll(37, dims=1).to(dev))
+    ep2 = fused(locs.to(dev), acts.roll(37, dims=1).to(dev))
     ep2.run_eager()
     torch.cuda.synchronize()
     assert ((ep2.reward - ep.reward).abs() <= 1e-5 * ep.reward.abs()).all()
 
 
 @pytest.mark.parametrize("bad", [5, 64 * 700 + 47, 64 * 700 + 48, 64 * 1000 + 63])
-def test_tsp_fused_large_batch_invalid_tour_flag(dev, bad):
+@LAYOUTS
+def test_tsp_fused_large_batch_invalid_tour_flag(dev, bad, fused):
     """Revisit detection at the full batch (1.33 rounds of resident tiles: first-round and
     tail tiles, low and high lanes), other instances' rewards unaffected."""
     b, n = 64 * 1024, 100
     locs = torch.rand(b, n, 2, generator=torch.Generator().manual_seed(7))
     acts = torch.arange(n).repeat(b, 1)
     acts[bad, 60] = 3  # node 3 twice, node 60 never
-    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep = fused(locs.to(dev), acts.to(dev))
     ep.run_eager()
     torch.cuda.synchronize()
     assert int(ep.status.item()) & 1
@@ -112,7 +123,8 @@ def test_tsp_fused_large_batch_invalid_tour_flag(dev, bad):
 
 
 @pytest.mark.parametrize("b", [768 * 64 + 40, 65536, 2 * 768 * 64 + 100])
-def test_tsp_fused_split_tail_tiles_final_state(dev, b):
+@LAYOUTS
+def test_tsp_fused_split_tail_tiles_final_state(dev, b, fused):
     """Batches past one resident round (768 full 64-instance tiles on 256 CUs) end in
     split tiles (32 instances, 8 step ranges).  Every row's final state and reward against
     the reference semantics computed on the CPU: mask = nodes absent from the action row
@@ -125,7 +137,7 @@ def test_tsp_fused_split_tail_tiles_final_state(dev, b):
     acts = torch.rand(b, n, generator=g).argsort(1)
     bad = torch.tensor([0, 49151, 49152, 49183, 49184, b - 1])
     acts[bad, 50] = acts[bad, 10]  # a revisit: the node at step 50 is never visited
-    ep = TSPFusedEpisode(locs.to(dev), acts.to(dev))
+    ep = fused(locs.to(dev), acts.to(dev))
     ep.run_eager()
     torch.cuda.synchronize()
     st = ep.final_state()

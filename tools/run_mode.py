@@ -51,7 +51,8 @@ def main():
         eps = []
         for r in range(n_rot):
             locs, acts = bench.tsp_inputs(65536, 100, 0, salt=r)
-            eps.append(TSPFusedEpisode(locs.to(dev), acts.to(dev), policy="teacher", check=True))
+            eps.append(TSPFusedEpisode(locs.to(dev), acts.to(dev), policy="teacher", check=True,
+                                       layout=os.environ.get("CO_TSP_LAYOUT", "rows")))
         sh = torch.cuda.current_stream(dev).cuda_stream
         cyc = itertools.cycle([e._bound for e in eps])
         wall, ev = bench.timed(lambda: next(cyc)(sh), a.k, 2, 1, dev)
