@@ -358,6 +358,9 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
 // next lane's first step (lane shuffle) and the closing edge, lane sums added in f64.
 // STATE = false: reward + validity only (co_tsp_reward on row-major actions, T == N);
 // coordinates of env e come from row e % LB (POMO multistart).
+#ifndef CO_ROWS_EPL112
+#define CO_ROWS_EPL112 7  // steps per lane for 96 < N <= 112 (16 lanes)
+#endif
 #ifndef CO_ROWS_DMA
 #define CO_ROWS_DMA 1  // the row kernel stages a wave's rows by LDS-DMA when it can
 #endif
@@ -402,11 +405,13 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
   unsigned char* s_w = s_rows + (DMA ? (size_t)w * 2 * half : 0);
   const float2* s_xy = reinterpret_cast<const float2*>(s_w);
   const int64_t* s_act = reinterpret_cast<const int64_t*>(s_w + half);
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
   const int nwords = (N + 31) >> 5;
   const int t0 = sl * EPL;
-  for (int64_t base = wid * GPW; base < B; base += nwaves * GPW) {
+  // one block of GPW instances per wave (the grid covers B: no loop, short live ranges)
+  {
+    const int64_t base = wid * GPW;
+    if (base >= B) return;
     const int64_t r = base + grp;
     const bool valid = r < B;
     const int64_t rr = valid ? r : 0;
@@ -427,8 +432,10 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
     // the lane's EPL actions: 16-byte vectors when the row is 16-byte aligned
     int64_t av[EPL];
     if constexpr (DMA) {
+      // branch-free: slots past N re-read step N-1 (in the staged block); their
+      // contributions are masked below
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) av[k] = (valid && t0 + k < N) ? s_act[grp * N + t0 + k] : 0;
+      for (int k = 0; k < EPL; ++k) av[k] = s_act[grp * N + (t0 + k < N ? t0 + k : N - 1)];
     } else if constexpr (VEC) {
 #pragma unroll
       for (int k = 0; k < EPL; k += 2) {
@@ -458,25 +465,31 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
     }
     const float2* lrow = DMA ? s_xy + grp * N : locs + (LB == B ? rr : rr % LB) * (int64_t)N;
     float2 p[EPL];
+    if constexpr (DMA) {  // node is always a valid LDS index
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) p[k] = (valid && t0 + k < N) ? lrow[node[k]] : make_float2(0.f, 0.f);
+      for (int k = 0; k < EPL; ++k) p[k] = lrow[node[k]];
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k)
+        p[k] = (valid && t0 + k < N) ? lrow[node[k]] : make_float2(0.f, 0.f);
+    }
     // the zeroed bitmap is visible to the group's other lanes (one wave, in order)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int k = 0; k < EPL; ++k)
-      if (valid && t0 + k < N)
-        __hip_atomic_fetch_or(&bits[node[k] >> 5], 1u << (node[k] & 31), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+    for (int k = 0; k < EPL; ++k)  // OR of 0 for slots past N: no branch
+      __hip_atomic_fetch_or(&bits[node[k] >> 5],
+                            (valid && t0 + k < N) ? 1u << (node[k] & 31) : 0u, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WAVEFRONT);
     // edges: within the lane, to the next lane's first step, and the closing edge
     float acc = 0.f;
 #pragma unroll
-    for (int k = 1; k < EPL; ++k)
-      if (t0 + k < N) {
-        const float dx = p[k].x - p[k - 1].x, dy = p[k].y - p[k - 1].y;
-        acc += __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-      }
+    for (int k = 1; k < EPL; ++k) {
+      const float dx = p[k].x - p[k - 1].x, dy = p[k].y - p[k - 1].y;
+      const float e = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+      acc += t0 + k < N ? e : 0.f;
+    }
     const float nx = __shfl_down(p[0].x, 1, G), ny = __shfl_down(p[0].y, 1, G);
     const float fx = __shfl(p[0].x, 0, G), fy = __shfl(p[0].y, 0, G);  // step 0
     const int tl = N - 1 - t0;  // this lane's slot of step N-1 (if 0 <= tl < EPL)
@@ -487,15 +500,17 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
         lx = p[k].x;
         ly = p[k].y;
       }
-    if (t0 + EPL < N) {  // edge (t0 + EPL - 1) -> (t0 + EPL), the next lane's first step
-      const float dx = nx - lx, dy = ny - ly;
-      acc += __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-    } else if (tl >= 0 && tl < EPL) {  // closing edge: step N-1 -> step 0 (roll by -1)
-      acc += edge_len(lx, ly, fx, fy);
+    {
+      // edge (t0 + EPL - 1) -> (t0 + EPL), the next lane's first step; or, on the lane
+      // holding step N-1, the closing edge N-1 -> 0 (roll by -1)
+      const bool cross = t0 + EPL < N, closing = !cross && tl >= 0 && tl < EPL;
+      const float tx = cross ? nx : fx, ty = cross ? ny : fy;
+      const float dx = tx - lx, dy = ty - ly;
+      const float e = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+      acc += (cross || closing) ? e : 0.f;
     }
-    double len = (double)acc;
-#pragma unroll
-    for (int d = G / 2; d >= 1; d >>= 1) len += __shfl_xor(len, d, G);
+    // lane sums (<= EPL edges) added across the group: f32, within the 1e-5 reward parity
+    const float len = grp_sum<G>(acc);
     // visited words: all N bits set <=> the N actions are a permutation (given in range)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -506,7 +521,7 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
     bad = grp_reduce<G>(bad, [](uint32_t x, uint32_t y) { return x | y; });
     const bool full = cnt == N;
     if (check && valid && sl == 0 && (bad || !full)) set_status(status, CO_ST_INVALID_TOUR);
-    if (!valid) continue;
+    if (!valid) return;
     if constexpr (STATE) {
       // action_mask row: byte c = node c not visited (all zero for a permutation)
       uint8_t* mrow = mask_out + r * (int64_t)N;
@@ -914,7 +929,7 @@ int launch_tsp_rows(int64_t B, int64_t N, const float2* l2, int64_t LB, const in
                       ((reinterpret_cast<uintptr_t>(acts) | reinterpret_cast<uintptr_t>(l2)) & 15) == 0;
 #define CO_ROWS(GG, EE)                                                                        \
   do {                                                                                         \
-    const dim3 grid(grid_for((B + 64 / GG - 1) / (64 / GG), 4, 256 * 32)), block(256);        \
+    const dim3 grid((unsigned)(((B + 64 / GG - 1) / (64 / GG) + 3) / 4)), block(256);          \
     const size_t dsh = 4 * tsp_rows_wave_bytes(64 / GG, (int)N);                               \
     if (dma_ok && (LB == B || LB % (64 / GG) == 0) && dsh <= 64 * 1024)                        \
       hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 2, STATE>), grid, block, dsh, s, B,   \
@@ -931,6 +946,7 @@ int launch_tsp_rows(int64_t B, int64_t N, const float2* l2, int64_t LB, const in
   } while (0)
   if (N <= 32) CO_ROWS(4, 8);
   else if (N <= 64) CO_ROWS(8, 8);
+  else if (N <= 16 * CO_ROWS_EPL112) CO_ROWS(16, CO_ROWS_EPL112);  // TSP-100: 7 steps a lane
   else if (N <= 128) CO_ROWS(16, 8);
   else if (N <= 256) CO_ROWS(32, 8);
   else if (N <= 512) CO_ROWS(64, 8);
