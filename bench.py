@@ -324,20 +324,32 @@ def cpu_baseline_tsp(locs, acts, episodes=3):
                       f"torch.set_num_threads({threads})"}
 
 
-def cpu_baseline_slap(b=2048, episodes=2):
+def cpu_baseline_slap(b=16384, episodes=2):
+    """The oracle's SLAP rollout at config 4's batch (the GPU modes' B=16,384): the
+    closest-free policy, the per-batch Python loop of slap/env.py:61-62 and the per-order
+    reward loop kept.  The instances' grid columns (identical for every instance: the
+    generator's analytic aisle grid) come from one generated block of 2,048 tiled to B --
+    the generator's own B x L Python loop (slap/generator.py:67-81) is not the workload
+    timed; freq and picklists are drawn for all B."""
     import numpy as np
 
     from oracle.envs import SLAPOracle, slap_closest_free_action
     from oracle.rollout import rollout
+    from oracle.td import TD
 
     torch.set_num_threads(cpu_threads())
     env = SLAPOracle(seed=1234)
     np.random.seed(1234)
-    gen = env.generate([b])
+    blk = min(b, 2048)
+    g0 = env.generate([blk])
+    reps = (b + blk - 1) // blk
+    gen = {k: torch.cat([g0[k]] * reps)[:b] for k in ("locs", "dist_mat", "depot_loc_dist",
+                                                    "assignment")}
+    gen["freq"] = env.freq_sampler.sample((b, env.n_products, 1))
+    gen["picklist"] = env.picklist([b])
+    gen = TD(gen, [b])
     times = []
     for _ in range(episodes + 1):
-        from oracle.td import TD
-
         td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
         t0 = time.perf_counter()
         rollout(env, td, slap_closest_free_action)

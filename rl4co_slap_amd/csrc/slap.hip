@@ -196,6 +196,166 @@ __global__ __launch_bounds__(WAVES * 64) void slap_reward_kernel(
   }
 }
 
+// SLAPEnv._get_reward (slap/env.py:131-143), G lanes per instance, 256/G instances per
+// workgroup, no loop: every load of the instance (its L coordinates, P assignment
+// entries and O*K picks, LU / PU / SU per lane, coalesced 8G- / 4G-byte row pieces) is
+// issued at once; coordinates and assignment land in the group's LDS, then each pick's
+// location (python's negative-index wrap of slap/env.py:139 and of the -1 of an
+// unassigned product) is looked up, its point stored, each order's closed tour summed
+// in pick order (edge_len, as torch's norm) by one lane per order, and the orders added
+// one by one in f32 by the group's lane 0 -- the reference's accumulation order.
+// LDS per instance: 8L + 4P + 8S + 4O bytes (16-byte rounded).
+__host__ __device__ inline int slap_rg_bytes(int L, int P, int S, int O) {
+  return (8 * L + ((4 * P + 7) & ~7) + 8 * S + 4 * O + 15) & ~15;
+}
+template <int G, int LU, int PU, int SU>
+__global__ __launch_bounds__(256) void slap_reward_group_kernel(
+    int64_t B, int L, int P, int O, int K, const int32_t* __restrict__ assignment,
+    const int64_t* __restrict__ picklist, const float2* __restrict__ locs,
+    float* __restrict__ reward, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_rg[];
+  const int S = O * K;
+  const int sl = threadIdx.x % G, gib = threadIdx.x / G;
+  const int64_t b = (int64_t)blockIdx.x * (256 / G) + gib;
+  const bool valid = b < B;
+  const int64_t rb = valid ? b : B - 1;  // dead groups mirror the last instance
+  unsigned char* base = s_rg + (size_t)gib * slap_rg_bytes(L, P, S, O);
+  float2* xy = reinterpret_cast<float2*>(base);
+  int32_t* asg = reinterpret_cast<int32_t*>(xy + L);
+  float2* pts = reinterpret_cast<float2*>(base + 8 * L + ((4 * P + 7) & ~7));
+  float* olen = reinterpret_cast<float*>(pts + S);
+  const float2* lrow = locs + rb * (int64_t)L;
+  const int32_t* arow = assignment + rb * (int64_t)P;
+  const int64_t* prow = picklist + rb * (int64_t)S;
+  float2 lv[LU];
+  int32_t av[PU];
+  int64_t pk[SU];
+#pragma unroll
+  for (int u = 0; u < LU; ++u) {
+    const int c = sl + G * u;
+    lv[u] = lrow[c < L ? c : L - 1];
+  }
+#pragma unroll
+  for (int u = 0; u < PU; ++u) {
+    const int c = sl + G * u;
+    av[u] = arow[c < P ? c : P - 1];
+  }
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int c = sl + G * u;
+    pk[u] = prow[c < S ? c : S - 1];
+  }
+#pragma unroll
+  for (int u = 0; u < LU; ++u)
+    if (sl + G * u < L) xy[sl + G * u] = lv[u];
+#pragma unroll
+  for (int u = 0; u < PU; ++u)
+    if (sl + G * u < P) asg[sl + G * u] = av[u];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  bool range = false;
+#pragma unroll
+  for (int u = 0; u < SU; ++u) {
+    const int sidx = sl + G * u;
+    if (sidx < S) {
+      int64_t pp = pk[u];
+      if (pp < 0) pp += P;
+      int64_t loc = 0;
+      if (pp < 0 || pp >= P) {
+        range = true;
+      } else {
+        loc = asg[pp];
+        if (loc < 0) loc += L;
+        if (loc < 0 || loc >= L) {
+          range = true;
+          loc = 0;
+        }
+      }
+      pts[sidx] = xy[loc];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int o = sl; o < O; o += G) {  // one lane per order: its closed tour in pick order
+    const float2* op = pts + o * K;
+    float len = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const float2 p0 = op[k], p1 = op[k + 1 == K ? 0 : k + 1];
+      len += edge_len(p0.x, p0.y, p1.x, p1.y);
+    }
+    olen[o] = len;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const bool bad = (__ballot(range && valid) != 0ull);
+  if (valid && sl == 0) {
+    float total = 0.f;  // orders added one by one (slap/env.py:135-142)
+    for (int o = 0; o < O; ++o) total += -olen[o];
+    reward[b] = total;
+  }
+  if (bad && threadIdx.x % 64 == 0) set_status(status, CO_ST_INDEX_RANGE);
+}
+
+// The reward for instances too large for the LDS staging of slap_reward_kernel (huge
+// L / order counts): one wave per instance, lane o walks order o's picks reading the
+// assignment and coordinates straight from global memory (L2), the orders added in order
+// from the lanes' registers.  Same results as the staged kernels.
+__global__ __launch_bounds__(256) void slap_reward_global_kernel(
+    int64_t B, int L, int P, int O, int K, const int32_t* __restrict__ assignment,
+    const int64_t* __restrict__ picklist, const float2* __restrict__ locs,
+    float* __restrict__ reward, int32_t* status) {
+  const int lane = lane_id();
+  const int64_t wpb = blockDim.x >> 6;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+       b += (int64_t)gridDim.x * wpb) {
+    const int64_t* prow = picklist + b * (int64_t)O * K;
+    const int32_t* arow = assignment + b * (int64_t)P;
+    const float2* lrow = locs + b * (int64_t)L;
+    bool range = false;
+    auto point = [&](int64_t pp) {
+      if (pp < 0) pp += P;
+      int64_t loc = 0;
+      if (pp < 0 || pp >= P) {
+        range = true;
+      } else {
+        loc = arow[pp];
+        if (loc < 0) loc += L;
+        if (loc < 0 || loc >= L) {
+          range = true;
+          loc = 0;
+        }
+      }
+      return lrow[loc];
+    };
+    float total = 0.f;
+    for (int o0 = 0; o0 < O; o0 += 64) {
+      const int o = o0 + lane;
+      float len = 0.f;
+      if (o < O) {
+        const float2 first = point(prow[(int64_t)o * K]);
+        float2 p0 = first;
+        for (int k = 1; k <= K; ++k) {
+          const float2 p1 = k == K ? first : point(prow[(int64_t)o * K + k]);
+          len += edge_len(p0.x, p0.y, p1.x, p1.y);
+          p0 = p1;
+        }
+      }
+      const int cnt = O - o0 < 64 ? O - o0 : 64;
+      for (int j = 0; j < cnt; ++j)
+        total += -__int_as_float(__builtin_amdgcn_readlane(__float_as_int(len), j));
+    }
+    if (lane == 0) reward[b] = total;
+    if (__any(range) && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
+  }
+}
+
+#ifndef CO_SLAP_RGROUP
+#define CO_SLAP_RGROUP 1
+#endif
+
 __global__ __launch_bounds__(256) void slap_closest_kernel(int64_t B, int L, const float* dist,
                                                            const uint8_t* mask, int64_t* out) {
   const int lane = lane_id();
@@ -336,12 +496,29 @@ extern "C" int co_slap_reward(int64_t B, int64_t L, int64_t P, int64_t O, int64_
   if (B == 0) return CO_OK;
   if (!assignment || !picklist || !locs || !reward) return CO_E_INVAL;
   if (reinterpret_cast<uintptr_t>(locs) & 7) return CO_E_ALIGN;
+  // lane group per instance (16 lanes, 16 instances per workgroup) when the instance's
+  // rows fit the per-lane register slots: L <= 128, P <= 32, S <= 128
+  if (CO_SLAP_RGROUP && L <= 16 * 8 && P <= 16 * 2 && O * K <= 16 * 8) {
+    const size_t shmem = (size_t)16 * slap_rg_bytes((int)L, (int)P, (int)(O * K), (int)O);
+    if (shmem <= 64 * 1024) {
+      hipLaunchKernelGGL((slap_reward_group_kernel<16, 8, 2, 8>), dim3((unsigned)((B + 15) / 16)),
+                         dim3(256), shmem, (hipStream_t)stream, B, (int)L, (int)P, (int)O,
+                         (int)K, assignment, picklist, reinterpret_cast<const float2*>(locs),
+                         reward, status);
+      return launch_status();
+    }
+  }
   // per wave, in float2 units: locations L, picks S, order lengths O (as floats, rounded
   // up to float2 with the assignment ints)
   const size_t per_wave = (size_t)(L + O * K + O + (P + 1) / 2) * sizeof(float2);
+  if (per_wave > 64 * 1024) {  // beyond the LDS staging: coordinates gathered from L2
+    hipLaunchKernelGGL(slap_reward_global_kernel, dim3(grid_for(B, 4, 256 * 32)), dim3(256), 0,
+                       (hipStream_t)stream, B, (int)L, (int)P, (int)O, (int)K, assignment,
+                       picklist, reinterpret_cast<const float2*>(locs), reward, status);
+    return launch_status();
+  }
   int waves = 4;
   while (waves > 1 && per_wave * waves > 64 * 1024) waves >>= 1;
-  if (per_wave > 64 * 1024) return CO_E_INVAL;
   const dim3 grid(grid_for(B, waves, 256 * 32));
   const size_t shmem = (size_t)waves * per_wave;
   const float2* l2 = reinterpret_cast<const float2*>(locs);

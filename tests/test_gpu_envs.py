@@ -449,3 +449,43 @@ def test_cvrp_reward_invalid_and_range(dev, step_major):
     bad[129, 3] = 21  # out of range
     _, st = _cvrp_reward_status(dev, locs, bad, dm, step_major)
     assert st & 1 and st & 8
+
+
+def _slap_reward_direct(dev, locs, assign, picks):
+    from rl4co_slap_amd import _native as nat
+
+    b, l, _ = locs.shape
+    p = assign.shape[1]
+    o, k = picks.shape[1], picks.shape[2]
+    lc, ac, pc = locs.contiguous().to(dev), assign.contiguous().to(dev), picks.contiguous().to(dev)
+    out = torch.empty(b, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    nat.call("co_slap_reward", b, l, p, o, k, nat.ptr(ac), nat.ptr(pc), nat.ptr(lc), nat.ptr(out),
+             nat.ptr(st), nat.stream_of(out))
+    torch.cuda.synchronize()
+    return out.cpu(), int(st.item())
+
+
+@pytest.mark.parametrize("b,l,p,o,k", [
+    (33, 100, 20, 20, 5),     # the lane-group kernel (16 instances per workgroup, tail block)
+    (5, 120, 32, 25, 5),      # its largest register slots (L <= 128, P <= 32, S <= 128)
+    (9, 300, 40, 30, 7),      # the LDS-staged wave-per-instance kernel
+    (3, 9000, 20, 20, 5),     # beyond the LDS staging: the global-gather kernel
+])
+def test_slap_reward_paths_vs_oracle(dev, b, l, p, o, k):
+    """co_slap_reward on every one of its three kernels, random coordinates, a partial
+    assignment (-1 wraps to the last slot) and picklists, against the oracle's
+    _get_reward (slap/env.py:131-143)."""
+    g = torch.Generator().manual_seed(l + p)
+    locs = torch.rand(b, l, 2, generator=g) * 10
+    assign = torch.randint(-1, l, (b, p), generator=g, dtype=torch.int64).to(torch.int32)
+    picks = torch.randint(0, p, (b, o, k), generator=g)
+    got, st = _slap_reward_direct(dev, locs, assign, picks)
+    ref = SLAPOracle._get_reward(TD({"assignment": assign, "picklist": picks, "locs": locs}, [b]),
+                                 None)
+    assert st == 0
+    assert_reward_close(got, ref)
+    # an out-of-range product index in a picklist is flagged (torch raises)
+    picks[0, 1, 2] = p + 3
+    _, st = _slap_reward_direct(dev, locs, assign, picks)
+    assert st & 8
