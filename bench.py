@@ -493,6 +493,7 @@ def main():
         # the drop-in API path (ConstructivePolicy + TSPEnv, one decode + one env launch
         # per step, Python TensorDict plumbing)
         modes["dropin_tsp100"] = bench_dropin(b, n, k, world, rank, dev)
+        modes["dropin_cvrp100"] = bench_dropin_cvrp(32768, 100, k, world, rank, dev)
         # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
         modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
         # the north star's "SLAP at batch 65,536": fused and stepwise
@@ -583,6 +584,8 @@ def annotate_modes(modes, n, world):
     per_step = {
         "tsp_stepwise_graph": lambda m: 2 * n + 50 + (16 * n + 4) / n,
         "dropin_tsp100": lambda m: 2 * n + 50 + 5 * n + 16 + (16 * n + 4) / n,
+        # decode: logits + mask read, action + logp written; the CVRP step as stepwise
+        "dropin_cvrp100": lambda m: 5 * (n + 1) + 12 + 16 * n + 50,
         "tsp_fused_nearest": lambda m: (17 * n + 30) / n,
         "slap_fused_closest": lambda m: 2754 / 20,
         "slap_fused_closest_b65536": lambda m: 2754 / 20,
@@ -692,39 +695,134 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
 
 
 def bench_dropin(b, n, k, world, rank, dev):
-    """The path an unchanged rl4co policy takes (VERDICT r1 item 7):
-    ``ConstructivePolicy(None, LogitsDecoder(stub)).forward(td, TSPEnv, greedy)`` at
-    TSP-100 B=65,536 -- per step the decode and the env step (greedy, logits from a fixed
-    HBM-resident [B, N] tensor: the stub decoder) as one co_tsp_decode_step launch
-    (TSPEnv.decode_and_step), the TensorDict plumbing in Python, the done poll only from
-    step N on (env lower bound),
-    then get_reward + validity and get_log_likelihood.  Also the host cost alone: the same
-    loop at B = 64, where the device work is negligible."""
+    """The path an unchanged rl4co policy takes (VERDICT r1 item 7, r2 item 4):
+    ``ConstructivePolicy(None, decoder).forward(td, TSPEnv, greedy)`` at TSP-100
+    B=65,536 -- per step the decode and the env step as one co_tsp_decode_step launch
+    (TSPEnv.decode_and_step through the native step glue), the TensorDict plumbing in
+    Python, the done poll only from step N on (env lower bound), then get_reward +
+    validity and get_log_likelihood.  Decoders: a stub (logits from a fixed HBM-resident
+    [B, N] tensor) and the AM-shaped pointer decoder of tests/am_pointer.py (glimpse +
+    pointer over cached projections, random init).  Reported beside them: the host cost
+    of one step of the loop (the same loop at B = 64, where the device work is
+    negligible) and the GPU time of the decode-fused kernel alone at B (HIP events)."""
+    from rl4co_slap_amd import _native
     from rl4co_slap_amd.envs import TSPEnv
+    from rl4co_slap_amd.rollout.constructive import ConstructivePolicy, LogitsDecoder
+    from rl4co_slap_amd.td import TensorDict
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+    from am_pointer import PointerDecoder
+
+    out = {}
+    for dec_name in ("stub", "am"):
+        for bb, kk in ((b, k), (64, 3 * k)):
+            locs, _ = tsp_inputs(bb, n, rank)
+            locs = locs.to(dev)
+            g = torch.Generator().manual_seed(7 + rank)
+            logits = torch.randn(bb, n, generator=g).to(dev)
+            env = TSPEnv(generator_params=dict(num_loc=n), device=dev)
+            dec = (LogitsDecoder(lambda td, lg=logits: lg) if dec_name == "stub"
+                   else PointerDecoder(locs, dev, cache=True))
+            pol = ConstructivePolicy(None, dec, env_name="tsp",
+                                     tanh_clipping=0.0 if dec_name == "stub" else 10.0)
+
+            def run():
+                td = env.reset(TensorDict({"locs": locs}, [bb]))
+                return pol(td, env, phase="test", decode_type="greedy")
+
+            wall, ev = timed(run, kk, 2, world, dev)
+            t = max_over_ranks(wall, world, dev)
+            key = "" if dec_name == "stub" else "am_"
+            if bb == b:
+                m = {"value": world * bb * n * kk / t, "ms_per_episode": t / kk * 1e3,
+                     "gpu_ms_per_episode": ev / kk * 1e3}
+                if dec_name == "stub":
+                    out.update(m)
+                    out.update({"batch_per_gpu": bb, "launches_per_step": 1,
+                                "done_polls_per_episode": 1,
+                                "path": "ConstructivePolicy.forward + TSPEnv"})
+                else:
+                    out["am_decoder"] = m
+            else:
+                out[key + "host_us_per_step_b64"] = t / kk / n * 1e6
+            del env, pol, dec
+    out["decode_fused_kernel_us"] = tsp_decode_step_kernel_us(b, n, dev)
+    out["host_below_kernel"] = out["host_us_per_step_b64"] < out["decode_fused_kernel_us"]
+    out["native_step_glue"] = _native.torchstep() is not None
+    return out
+
+
+def tsp_decode_step_kernel_us(b, n, dev, reps=50):
+    """GPU time of one co_tsp_decode_step launch (certified greedy, the drop-in default)
+    at B x N: a mid-episode state (half the nodes visited), HIP events over reps
+    launches on the launching stream."""
+    from rl4co_slap_amd import _native
+
+    g = torch.Generator().manual_seed(3)
+    logits = torch.randn(b, n, generator=g).to(dev)
+    mask = (torch.rand(b, n, generator=g) < 0.5).to(dev)
+    mask[:, 0] = True
+    i = torch.full((b, 1), n // 2, dtype=torch.int64, device=dev)
+    first = torch.zeros(b, dtype=torch.int64, device=dev)
+    outs = [torch.empty(b, dtype=torch.int64, device=dev), torch.empty(b, device=dev),
+            torch.empty((b, n), dtype=torch.bool, device=dev),
+            torch.empty((b, 1), dtype=torch.int64, device=dev),
+            torch.empty(b, dtype=torch.int64, device=dev),
+            torch.empty(b, dtype=torch.bool, device=dev), torch.empty(b, dtype=torch.bool,
+                                                                        device=dev)]
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    launch = _native.bind("co_tsp_decode_step", b, n, logits.data_ptr(), n, mask.data_ptr(),
+                          0.0, 1.0, _native.DECODE_CERTIFIED, None, outs[0].data_ptr(),
+                          outs[1].data_ptr(), 0, 0, outs[2].data_ptr(), i.data_ptr(),
+                          outs[3].data_ptr(), first.data_ptr(), outs[4].data_ptr(), 0,
+                          outs[5].data_ptr(), outs[6].data_ptr(), None, st.data_ptr())
+    _, ev = timed(lambda: launch(sh), reps, 5, 1, dev)
+    return ev / reps * 1e6
+
+
+def bench_dropin_cvrp(b, n, k, world, rank, dev):
+    """The drop-in path on CVRP-100 (SURVEY.md 8d config 3 data): ConstructivePolicy +
+    CVRPEnv, greedy on a stub decoder (a fixed HBM-resident [B, N+1] logits tensor whose
+    masked argmax is the decoded action), per step one co_decode_step + one co_cvrp_step
+    launch through the native step glue; the episode length is data dependent (polls
+    resume once the env's lower bound N+1 is reached).  Plus the host cost per step at
+    B = 64 and the per-step GPU time of the two kernels (HIP events over the episode)."""
+    from rl4co_slap_amd.envs import CVRPEnv
     from rl4co_slap_amd.rollout.constructive import ConstructivePolicy, LogitsDecoder
     from rl4co_slap_amd.td import TensorDict
 
     out = {}
     for bb, kk in ((b, k), (64, 3 * k)):
-        locs, _ = tsp_inputs(bb, n, rank)
-        locs = locs.to(dev)
-        g = torch.Generator().manual_seed(7 + rank)
-        logits = torch.randn(bb, n, generator=g).to(dev)
-        env = TSPEnv(generator_params=dict(num_loc=n), device=dev)
-        pol = ConstructivePolicy(None, LogitsDecoder(lambda td: logits), env_name="tsp")
+        torch.manual_seed(1234 + rank)
+        la = torch.rand(bb, n + 1, 2)
+        dm = ((torch.rand(bb, n) * 9).int() + 1).float() / 50.0
+        data = {"depot": la[:, 0].contiguous().to(dev), "locs": la[:, 1:].contiguous().to(dev),
+                "demand": dm.to(dev)}
+        g = torch.Generator().manual_seed(17 + rank)
+        logits = torch.randn(bb, n + 1, generator=g).to(dev)
+        env = CVRPEnv(generator_params=dict(num_loc=n), device=dev)
+        pol = ConstructivePolicy(None, LogitsDecoder(lambda td: logits), env_name="cvrp")
+        steps = []
 
         def run():
-            td = env.reset(TensorDict({"locs": locs}, [bb]))
-            return pol(td, env, phase="test", decode_type="greedy")
+            td = env.reset(TensorDict(dict(data), [bb]))
+            r = pol(td, env, phase="test", decode_type="greedy", return_actions=True)
+            steps.append(r["actions"].shape[1])
+            return r
 
-        wall, _ = timed(run, kk, 2, world, dev)
+        wall, ev = timed(run, kk, 2, world, dev)
         t = max_over_ranks(wall, world, dev)
+        T = steps[-1]
         if bb == b:
-            out = {"value": world * bb * n * kk / t, "ms_per_episode": t / kk * 1e3,
-                   "batch_per_gpu": bb, "launches_per_step": 1,
-                   "done_polls_per_episode": 1, "path": "ConstructivePolicy.forward + TSPEnv"}
+            out.update({"value": world * bb * T * kk / t, "ms_per_episode": t / kk * 1e3,
+                        "gpu_ms_per_episode": ev / kk * 1e3, "episode_steps": T,
+                        "gpu_us_per_step": ev / kk / T * 1e6, "batch_per_gpu": bb,
+                        "launches_per_step": 2,
+                        "path": "ConstructivePolicy.forward + CVRPEnv"})
         else:
-            out["host_us_per_step_b64"] = t / kk / n * 1e6
+            out["host_us_per_step_b64"] = t / kk / T * 1e6
+    out["host_below_kernels"] = out["host_us_per_step_b64"] < out["gpu_us_per_step"]
     return out
 
 

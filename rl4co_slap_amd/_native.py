@@ -282,6 +282,65 @@ def _fastcall():
     return _fast
 
 
+TORCHSTEP_PATH = os.path.join(_HERE, "_lib", "_co_torchstep" + (
+    __import__("sysconfig").get_config_var("EXT_SUFFIX") or ".so"))
+_tstep = None  # the loaded glue module once tried, False when unavailable
+
+
+class _TorchStep:
+    """The drop-in loop's step glue (csrc/pycall/co_torchstep.cpp): per fused step, output
+    allocation + the C-ABI launch in one call.  ``addr`` holds the entry points' addresses
+    in the loaded device library (the glue calls through them; it links no kernels)."""
+
+    def __init__(self, mod):
+        self.mod = mod
+        lib = load()
+        addr = lambda n: ctypes.cast(getattr(lib, n), ctypes.c_void_p).value  # noqa: E731
+        self._tsp_decode_step = addr("co_tsp_decode_step")
+        self._decode_step = addr("co_decode_step")
+        self._cvrp_step = addr("co_cvrp_step")
+
+    def tsp_decode_step(self, *args):
+        return self.mod.tsp_decode_step(self._tsp_decode_step, *args)
+
+    def decode_step(self, *args):
+        return self.mod.decode_step(self._decode_step, *args)
+
+    def cvrp_step(self, *args):
+        return self.mod.cvrp_step(self._cvrp_step, *args)
+
+
+def torchstep():
+    """The step glue, or None (built against another torch / interpreter, not built, or
+    ``CO_NO_TORCHSTEP`` set): callers then take their Python path, same results."""
+    global _tstep
+    if _tstep is not None:
+        return _tstep or None
+    _tstep = False
+    if os.environ.get("CO_NO_TORCHSTEP") or not os.path.exists(TORCHSTEP_PATH):
+        return None
+    try:
+        import importlib.machinery
+        import importlib.util
+
+        loader = importlib.machinery.ExtensionFileLoader("_co_torchstep", TORCHSTEP_PATH)
+        spec = importlib.util.spec_from_file_location("_co_torchstep", TORCHSTEP_PATH,
+                                                      loader=loader)
+        mod = importlib.util.module_from_spec(spec)
+        loader.exec_module(mod)
+        _tstep = _TorchStep(mod)
+    except Exception as e:  # e.g. undefined torch symbols: a build for another torch
+        warnings.warn(f"rl4co_slap_amd: step glue module unusable ({e}); using the Python "
+                      "step path", RuntimeWarning, stacklevel=2)
+        return None
+    return _tstep
+
+
+def check_rc(name, rc):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
+
+
 def call(name, *args):
     fast = _fast if _fast else _fastcall()
     if args and args[-1] is HOST:

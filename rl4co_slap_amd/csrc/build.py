@@ -89,6 +89,8 @@ def build(force=False, verbose: bool = False) -> str:
         if (not os.path.exists(FASTCALL_LIB)
                 or os.path.getmtime(FASTCALL_LIB) < os.path.getmtime(FASTCALL_SRC)):
             build_fastcall(verbose=verbose)
+        if _torchstep_stale():
+            build_torchstep(verbose=verbose)
         return LIB
     os.makedirs(OUT_DIR, exist_ok=True)
     obj_dir = os.path.join(OUT_DIR, "obj")
@@ -124,6 +126,7 @@ def build(force=False, verbose: bool = False) -> str:
     os.replace(tmp, LIB)
     build_host(verbose=verbose)
     build_fastcall(verbose=verbose)
+    build_torchstep(verbose=verbose)
     return LIB
 
 
@@ -162,6 +165,44 @@ def build_fastcall(verbose: bool = False) -> str:
     subprocess.run(cmd, check=True)
     os.replace(FASTCALL_LIB + ".tmp", FASTCALL_LIB)
     return FASTCALL_LIB
+
+
+TORCHSTEP_SRC = os.path.join(HERE, "pycall", "co_torchstep.cpp")
+TORCHSTEP_LIB = os.path.join(OUT_DIR, "_co_torchstep" + _ext_suffix())
+
+
+def _torchstep_stale() -> bool:
+    if not os.path.exists(TORCHSTEP_LIB):
+        return True
+    t = os.path.getmtime(TORCHSTEP_LIB)
+    return any(os.path.getmtime(d) > t for d in (TORCHSTEP_SRC, os.path.join(ROOT, "include",
+                                                                           "co_env.h")))
+
+
+def build_torchstep(verbose: bool = False) -> str:
+    """The drop-in loop's step glue (csrc/pycall/co_torchstep.cpp): a CPython module
+    against this torch's headers and libraries (g++, no device code).  Optional: without
+    it the env steps take their Python path."""
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension
+
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    libdir = cpp_extension.library_paths()[0]
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__=1",
+           "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={int(torch._C._GLIBCXX_USE_CXX11_ABI)}",
+           "-I", sysconfig.get_paths()["include"], "-I", "/opt/rocm/include",
+           "-I", os.path.join(ROOT, "include")]
+    for inc in cpp_extension.include_paths():
+        cmd += ["-isystem", inc]
+    cmd += ["-o", TORCHSTEP_LIB + ".tmp", TORCHSTEP_SRC, "-L", libdir, "-Wl,-rpath," + libdir,
+            "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(TORCHSTEP_LIB + ".tmp", TORCHSTEP_LIB)
+    return TORCHSTEP_LIB
 
 
 def build_host(verbose: bool = False, out: str = HOST_LIB, extra=()) -> str:

@@ -125,6 +125,40 @@ __device__ __forceinline__ uint32_t grp_reduce(uint32_t v, Op op) {
   return v;
 }
 
+// f64 sum over the group (each stage moves the two halves): exact enough that the f32
+// rounding of a sum of f32 terms does not depend on the terms' order
+template <int RL>
+__device__ __forceinline__ double grp_sum_f64(double v) {
+  uint32_t lo = (uint32_t)__double_as_longlong(v), hi = (uint32_t)(__double_as_longlong(v) >> 32);
+  auto join = [](uint32_t l, uint32_t h) {
+    return __longlong_as_double((long long)(((uint64_t)h << 32) | l));
+  };
+#define CO_DPP_F64(C)                                   \
+  {                                                     \
+    v = v + join(dpp_u<C>(lo), dpp_u<C>(hi));           \
+    lo = (uint32_t)__double_as_longlong(v);             \
+    hi = (uint32_t)(__double_as_longlong(v) >> 32);     \
+  }
+  if (RL >= 2) CO_DPP_F64(0xB1);
+  if (RL >= 4) CO_DPP_F64(0x4E);
+  if (RL >= 8) CO_DPP_F64(0x141);
+  if (RL >= 16) CO_DPP_F64(0x140);
+#undef CO_DPP_F64
+  if (RL >= 32) {
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = join(rl[0], rh[0]) + join(rl[1], rh[1]);
+    lo = (uint32_t)__double_as_longlong(v);
+    hi = (uint32_t)(__double_as_longlong(v) >> 32);
+  }
+  if (RL >= 64) {
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = join(rl[0], rh[0]) + join(rl[1], rh[1]);
+  }
+  return v;
+}
+
 template <int RL>
 __device__ __forceinline__ float grp_max(float v) {
   return __uint_as_float(grp_reduce<RL>(__float_as_uint(v), [](uint32_t x, uint32_t y) {

@@ -197,8 +197,9 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
     py = fy = p0.y;
     // A batch is one basic block: U LDS coordinate reads, U no-return visited-bit clears
     // (a revisit shows in the final visited words: N steps over N nodes clear them all
-    // exactly when the actions are a permutation), U independent edge lengths summed in
-    // f32, one f64 add -- one LDS round trip per batch.  Edge lengths use the hardware
+    // exactly when the actions are a permutation), U independent edge lengths, each added
+    // in f64 (the f32 length then does not depend on the order: a tour and its reverse
+    // score the same) -- one LDS round trip per batch.  Edge lengths use the hardware
     // v_sqrt_f32 (<= 1 ulp; reward parity is 1e-5 relative).
     auto run = [&](const int64_t (&src)[U], int cnt) {  // cnt: steps used (uniform)
       int av[U];
@@ -223,16 +224,14 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
       // keep the batch's LDS operations issued back to back (the scheduler otherwise
       // splits the reads into groups with a full wait between them)
       __builtin_amdgcn_sched_barrier(0);
-      float acc = 0.f;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (u < cnt) {
           const float ox = u ? qq[u - 1].x : px, oy = u ? qq[u - 1].y : py;
           const float dx = qq[u].x - ox, dy = qq[u].y - oy;
-          acc += __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+          len += (double)__builtin_amdgcn_sqrtf(dx * dx + dy * dy);
         }
       }
-      len += (double)acc;
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (u + 1 == cnt) {
@@ -482,13 +481,15 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
       __hip_atomic_fetch_or(&bits[node[k] >> 5],
                             (valid && t0 + k < N) ? 1u << (node[k] & 31) : 0u, __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_WAVEFRONT);
-    // edges: within the lane, to the next lane's first step, and the closing edge
-    float acc = 0.f;
+    // edges: within the lane, to the next lane's first step, and the closing edge; summed
+    // in f64 so the f32 tour length does not depend on the summation order (a tour and its
+    // reverse get the same reward, as the step-major kernel's f64 accumulation gives)
+    double acc = 0.0;
 #pragma unroll
     for (int k = 1; k < EPL; ++k) {
       const float dx = p[k].x - p[k - 1].x, dy = p[k].y - p[k - 1].y;
       const float e = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-      acc += t0 + k < N ? e : 0.f;
+      acc += t0 + k < N ? (double)e : 0.0;
     }
     const float nx = __shfl_down(p[0].x, 1, G), ny = __shfl_down(p[0].y, 1, G);
     const float fx = __shfl(p[0].x, 0, G), fy = __shfl(p[0].y, 0, G);  // step 0
@@ -507,10 +508,9 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
       const float tx = cross ? nx : fx, ty = cross ? ny : fy;
       const float dx = tx - lx, dy = ty - ly;
       const float e = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-      acc += (cross || closing) ? e : 0.f;
+      acc += (cross || closing) ? (double)e : 0.0;
     }
-    // lane sums (<= EPL edges) added across the group: f32, within the 1e-5 reward parity
-    const float len = grp_sum<G>(acc);
+    const float len = (float)grp_sum_f64<G>(acc);
     // visited words: all N bits set <=> the N actions are a permutation (given in range)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -115,6 +115,13 @@ class CVRPEnv(RL4COEnvBase):
         action = td["action"]
         demand, used, vcap, visited = (td["demand"], td["used_capacity"], td["vehicle_capacity"],
                                        td["visited"])
+        ts = nat.torchstep()
+        r = ts.cvrp_step(action, demand, used, vcap, visited) if ts is not None else None
+        if r is not None:  # output allocation + launch in one native call
+            if type(r) is int:
+                nat.check_rc("co_cvrp_step", r)
+            used_out, visited_out, cur, done, reward, mask = r
+            return self._after_step(td, used_out, visited_out, cur, done, reward, mask)
         nat.require_device(action, demand, used, vcap, visited)
         if action.dtype != torch.int64:
             action = action.long()
@@ -132,6 +139,9 @@ class CVRPEnv(RL4COEnvBase):
         nat.call("co_cvrp_step", b, n, nat.ptr(action), nat.ptr(demand), nat.ptr(used),
                  nat.ptr(used_out), nat.ptr(vcap), nat.ptr(visited), nat.ptr(visited_out),
                  nat.ptr(cur), nat.ptr(done), nat.ptr(reward), nat.ptr(mask), None, None, s)
+        return self._after_step(td, used_out, visited_out, cur, done, reward, mask)
+
+    def _after_step(self, td, used_out, visited_out, cur, done, reward, mask):
         lb = self._known_lb(td["visited"])
         if lb is not None:  # a step marks at most one more node visited
             self._remember_lb(visited_out, lb - 1)

@@ -119,6 +119,17 @@ class TSPEnv(RL4COEnvBase):
         take = 1 if known == 0 else 0
         if not take and first_in is None:
             return None
+        ts = nat.torchstep()
+        if ts is not None:  # output allocation + launch in one native call
+            r = ts.tsp_decode_step(logits, mask, i, None if take else first_in, action_in,
+                                   status, float(tanh_clipping), float(temperature), mode, seed,
+                                   offset, take)
+            if r is not None:
+                if type(r) is int:
+                    nat.check_rc("co_tsp_decode_step", r)
+                act, logp, mask_out, i_out, first_out, done, reward = r
+                return self._after_decode_step(td, key, action_in, act, logp, mask_out, i_out,
+                                               first_out, done, reward, known)
         b, n = mask.shape
         if logits.shape != (b, n) or n > 2048:  # long rows: co_decode_step's row kernel
             return None
@@ -140,6 +151,11 @@ class TSPEnv(RL4COEnvBase):
                  nat.ptr(logp), seed, offset, nat.ptr(mask_out), nat.ptr(i), nat.ptr(i_out),
                  nat.ptr(first_in), nat.ptr(first_out), take, nat.ptr(done), nat.ptr(reward),
                  None, nat.ptr(status), s)
+        return self._after_decode_step(td, key, action_in, act, logp, mask_out, i_out,
+                                       first_out, done, reward, known)
+
+    def _after_decode_step(self, td, key, action_in, act, logp, mask_out, i_out, first_out,
+                           done, reward, known):
         sel = action_in if action_in is not None else act
         self._remember_i(i_out, known + 1)
         lb = self._known_lb(td["action_mask"])

@@ -55,8 +55,19 @@ def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, act
                 top_p: float = 0.0, math: str = "exact"):
     """One fused decode step.  Returns ``(action[B], logp[B], full_logprobs or None)``.
     ``math`` selects the decode math (``_MATH`` above)."""
-    nat.require_device(logits, mask, action)
     flags = math_flags(math)
+    mword = _MODES[mode] | flags
+    if seed is None:
+        seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
+    ts = nat.torchstep() if top_k <= 0 and top_p <= 0 else None
+    if ts is not None:  # output allocation + launch in one native call (device tensors)
+        r = ts.decode_step(logits, mask, action, status, float(tanh_clipping),
+                           float(temperature), mword, seed, offset, return_full)
+        if r is not None:
+            if type(r) is int:
+                nat.check_rc("co_decode_step", r)
+            return r
+    nat.require_device(logits, mask, action)
     if logits.dtype != torch.float32:
         logits = logits.float()
     if logits.stride(-1) != 1:
@@ -70,8 +81,6 @@ def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, act
     full = torch.empty((b, n), dtype=torch.float32, device=dev) if return_full else None
     if action is not None:
         action = action.long().contiguous()
-    if seed is None:
-        seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
     if top_k > 0 or top_p > 0:
         assert top_p <= 1.0, "top-p should be in (0, 1]."
         nat.call("co_decode_step_ex", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
@@ -80,7 +89,7 @@ def decode_step(logits, mask, mode: str, temperature=1.0, tanh_clipping=0.0, act
                  seed, offset, nat.ptr(status), nat.stream_of(logits))
     else:
         nat.call("co_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
-                 float(tanh_clipping), float(temperature), _MODES[mode] | flags,
+                 float(tanh_clipping), float(temperature), mword,
                  nat.ptr(action), nat.ptr(act_out), nat.ptr(logp), nat.ptr(full), seed, offset, nat.ptr(status),
                  nat.stream_of(logits))
     return act_out, logp, full

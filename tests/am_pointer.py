@@ -16,8 +16,10 @@ H, HEADS = 32, 4
 class PointerDecoder(nn.Module):
     """A small attention-model decoder (random init, eval mode, on the device)."""
 
-    def __init__(self, locs_bn2, dev, depot_env=False):
+    def __init__(self, locs_bn2, dev, depot_env=False, cache=False):
         super().__init__()
+        self.cache = cache  # precompute the key / value / logit-key projections once (the
+        self._kvl = None    # AM's _precompute_cache, am/decoder.py:138-160)
         g = torch.Generator().manual_seed(5)
 
         def lin(i, o):
@@ -41,20 +43,34 @@ class PointerDecoder(nn.Module):
         """am/decoder.py:162-200 shaped: glimpse + pointer; rows e of a multistart batch
         use instance e % B's embeddings (the AM batchifies its cached embeddings)."""
         e = first.shape[0]
-        h = self.h[torch.arange(e, device=self.h.device) % self.b]  # [E, N, H]
-        n = h.shape[1]
-        hf = h.gather(1, first.reshape(e, 1, 1).expand(e, 1, H)).squeeze(1)
-        hc = h.gather(1, cur.reshape(e, 1, 1).expand(e, 1, H)).squeeze(1)
+        n = self.h.shape[1]
+        if self.cache and self._kvl is not None and self._kvl[0].shape[0] == e:
+            rows = self._rows  # the cached projections stand for h: gather the two rows only
+            hf, hc = self.h[rows, first.reshape(e)], self.h[rows, cur.reshape(e)]
+            h = None
+        else:
+            self._rows = torch.arange(e, device=self.h.device) % self.b
+            h = self.h[self._rows]  # [E, N, H]
+            hf = h.gather(1, first.reshape(e, 1, 1).expand(e, 1, H)).squeeze(1)
+            hc = h.gather(1, cur.reshape(e, 1, 1).expand(e, 1, H)).squeeze(1)
         ctx = torch.cat([hf, hc], -1)
         if not self.depot_env:  # TSP context: the placeholder before the first step
             ctx = torch.where((i.reshape(e, 1) == 0), self.placeholder.expand(e, -1), ctx)
         q = self.wq(ctx).view(e, HEADS, 1, H // HEADS)
-        k = self.wk(h).view(e, n, HEADS, H // HEADS).transpose(1, 2)
-        v = self.wv(h).view(e, n, HEADS, H // HEADS).transpose(1, 2)
-        att = (q @ k.transpose(-1, -2)) / math.sqrt(H // HEADS)
+        if self.cache:
+            if self._kvl is None or self._kvl[0].shape[0] != e:
+                self._kvl = (self.wk(h).view(e, n, HEADS, H // HEADS).permute(0, 2, 3, 1),
+                             self.wv(h).view(e, n, HEADS, H // HEADS).transpose(1, 2),
+                             self.wl(h).transpose(1, 2).contiguous())
+            kt, v, lt = self._kvl
+        else:
+            kt = self.wk(h).view(e, n, HEADS, H // HEADS).permute(0, 2, 3, 1)
+            v = self.wv(h).view(e, n, HEADS, H // HEADS).transpose(1, 2)
+            lt = self.wl(h).transpose(1, 2)
+        att = (q @ kt) / math.sqrt(H // HEADS)
         att = att.masked_fill(~mask.view(e, 1, 1, n), float("-inf"))
         glimpse = self.wo((att.softmax(-1) @ v).reshape(e, H))
-        return (glimpse.unsqueeze(1) @ self.wl(h).transpose(1, 2)).squeeze(1) / math.sqrt(H)
+        return (glimpse.unsqueeze(1) @ lt).squeeze(1) / math.sqrt(H)
 
     # ConstructiveDecoder interface (constructive/base.py:43-86)
     def forward(self, td, hidden=None, num_starts: int = 0):

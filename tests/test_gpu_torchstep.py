@@ -1,0 +1,126 @@
+"""The drop-in loop's step glue (csrc/pycall/co_torchstep.cpp): the same launches as the
+Python step path with the outputs allocated natively.  Every output must equal the Python
+path's bit for bit (same kernels, same arguments), the glue must be the path that runs on
+the GPU box, and it must step aside (return None) whenever its operands do not fit."""
+import pytest
+import torch
+
+from rl4co_slap_amd import TensorDict
+from rl4co_slap_amd import _native as nat
+from rl4co_slap_amd.envs import CVRPEnv, TSPEnv
+from rl4co_slap_amd.rollout import ConstructivePolicy, LogitsDecoder
+
+from am_pointer import PointerDecoder
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def python_path():
+    """Run the body with the glue disabled (the Python step path), then restore it."""
+    saved = nat._tstep
+
+    class _Off:
+        def __enter__(self):
+            nat._tstep = False
+
+        def __exit__(self, *exc):
+            nat._tstep = saved
+
+    return _Off
+
+
+def test_glue_is_loaded(dev):
+    ts = nat.torchstep()
+    assert ts is not None, "the step glue module must load on the GPU box"
+
+
+def _run(env_cls, gen, dev, decode_type, dec_fn, name, **kw):
+    env = env_cls(generator_params=dict(num_loc=kw.pop("n")), device=dev)
+    td = env.reset(TensorDict({k: v.clone().to(dev) for k, v in gen.items()},
+                              [gen[next(iter(gen))].shape[0]]))
+    torch.manual_seed(77)
+    pol = ConstructivePolicy(None, dec_fn, env_name=name, tanh_clipping=10.0)
+    return pol(td, env, phase="test", decode_type=decode_type, return_actions=True, **kw)
+
+
+def _same(a, b):
+    for k in ("actions", "reward", "log_likelihood"):
+        x, y = a[k], b[k]
+        assert x.dtype == y.dtype and x.shape == y.shape, k
+        assert torch.equal(x.view(torch.int32) if x.is_floating_point() else x,
+                           y.view(torch.int32) if y.is_floating_point() else y), k
+
+
+@pytest.mark.parametrize("decode_type", ["greedy", "sampling", "multistart_greedy"])
+def test_tsp_glue_equals_python_path(dev, python_path, decode_type):
+    b, n = 96, 30
+    gen = {"locs": torch.rand(b, n, 2, generator=torch.Generator().manual_seed(4))}
+    dec = PointerDecoder(gen["locs"], dev)
+    glue = _run(TSPEnv, gen, dev, decode_type, dec, "tsp", n=n)
+    with python_path():
+        ref = _run(TSPEnv, gen, dev, decode_type, dec, "tsp", n=n)
+    _same(glue, ref)
+
+
+@pytest.mark.parametrize("decode_type", ["greedy", "sampling"])
+def test_cvrp_glue_equals_python_path(dev, python_path, decode_type):
+    b, n = 64, 20
+    g = torch.Generator().manual_seed(8)
+    gen = {"depot": torch.rand(b, 2, generator=g), "locs": torch.rand(b, n, 2, generator=g),
+           "demand": ((torch.rand(b, n, generator=g) * 9).int() + 1).float() / 30.0}
+    dec = PointerDecoder(torch.cat([gen["depot"][:, None], gen["locs"]], 1), dev,
+                         depot_env=True)
+    glue = _run(CVRPEnv, gen, dev, decode_type, dec, "cvrp", n=n)
+    with python_path():
+        ref = _run(CVRPEnv, gen, dev, decode_type, dec, "cvrp", n=n)
+    _same(glue, ref)
+
+
+def test_glue_evaluate_mode_and_logits_views(dev, python_path):
+    """Evaluate mode (action_in) and a strided logits view (row stride > N) take the glue
+    with the same results; int32 actions make it step aside (the Python path casts)."""
+    b, n = 40, 25
+    locs = torch.rand(b, n, 2, generator=torch.Generator().manual_seed(9))
+    wide = torch.randn(b, n + 7, generator=torch.Generator().manual_seed(10)).to(dev)
+    acts = torch.rand(b, n, generator=torch.Generator().manual_seed(11)).argsort(1).to(dev)
+    outs = []
+    for off in (False, True):
+        for a in (acts, acts.int()):
+            env = TSPEnv(generator_params=dict(num_loc=n), device=dev)
+            td = env.reset(TensorDict({"locs": locs.to(dev)}, [b]))
+            pol = ConstructivePolicy(None, LogitsDecoder(lambda t: wide[:, :n]), env_name="tsp")
+            if off:
+                with python_path():
+                    outs.append(pol(td, env, actions=a, return_actions=True))
+            else:
+                outs.append(pol(td, env, actions=a, return_actions=True))
+    _same(outs[0], outs[2])  # int64 actions: glue vs Python path
+    _same(outs[1], outs[3])  # int32 actions: both on the Python path
+    assert torch.equal(outs[0]["log_likelihood"], outs[1]["log_likelihood"])
+
+
+def test_glue_steps_aside(dev):
+    ts = nat.torchstep()
+    b, n = 8, 10
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    logits = torch.randn(b, n, device=dev)
+    mask = torch.ones(b, n, dtype=torch.bool, device=dev)
+    i = torch.zeros(b, 1, dtype=torch.int64, device=dev)
+    # CPU operands, half logits, a non-contiguous mask: None (the Python path handles them)
+    assert ts.tsp_decode_step(logits.cpu(), mask.cpu(), i.cpu(), None, None, st.cpu(), 0.0, 1.0,
+                              0, 0, 0, 1) is None
+    assert ts.tsp_decode_step(logits.half(), mask, i, None, None, st, 0.0, 1.0, 0, 0, 0,
+                              1) is None
+    assert ts.decode_step(logits, mask.t().contiguous().t(), None, st, 0.0, 1.0, 0, 0, 0,
+                          False) is None
+    assert ts.decode_step(logits.cpu(), None, None, None, 0.0, 1.0, 0, 0, 0, False) is None
+    # a bad mode is the C ABI's error code, raised by the caller
+    rc = ts.decode_step(logits, mask, None, st, 0.0, 1.0, 7, 0, 0, False)
+    assert type(rc) is int and rc != 0
+    # outputs are distinct, 256-byte aligned regions
+    r = ts.tsp_decode_step(logits, mask, i, None, None, st, 0.0, 1.0, 0, 0, 0, 1)
+    ptrs = sorted(t.data_ptr() for t in r)
+    assert len(set(ptrs)) == len(ptrs) and all(p % 256 == 0 for p in ptrs)
+    torch.cuda.synchronize()
+    assert int(st.item()) == 0

@@ -1,6 +1,6 @@
 """Run one bench.py mode alone (for rocprofv3 kernel traces of a single path).
 
-    python tools/run_mode.py cvrp|slap|slap65k|pomo|dropin|tsp|gen [--k K]
+    python tools/run_mode.py cvrp|slap|slap65k|pomo|dropin|dropin_cvrp|tsp|gen [--k K]
 """
 import argparse
 import json
@@ -38,6 +38,8 @@ def main():
         out = {k: round(v["kernel_us"], 3) for k, v in out.items()}
     elif a.mode == "dropin":
         out = bench.bench_dropin(65536, 100, a.k, 1, 0, dev)
+    elif a.mode == "dropin_cvrp":
+        out = bench.bench_dropin_cvrp(32768, 100, a.k, 1, 0, dev)
     elif a.mode == "pomo":
         out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev)
     elif a.mode == "pomo_cert":
