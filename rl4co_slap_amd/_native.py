@@ -289,25 +289,21 @@ _tstep = None  # the loaded glue module once tried, False when unavailable
 
 class _TorchStep:
     """The drop-in loop's step glue (csrc/pycall/co_torchstep.cpp): per fused step, output
-    allocation + the C-ABI launch in one call.  ``addr`` holds the entry points' addresses
-    in the loaded device library (the glue calls through them; it links no kernels)."""
+    allocation + the C-ABI launch in one call.  Each function is bound to its entry point's
+    address in the loaded device library (the glue calls through it; it links no kernels)."""
 
     def __init__(self, mod):
-        self.mod = mod
+        import functools
+
         lib = load()
-        addr = lambda n: ctypes.cast(getattr(lib, n), ctypes.c_void_p).value  # noqa: E731
-        self._tsp_decode_step = addr("co_tsp_decode_step")
-        self._decode_step = addr("co_decode_step")
-        self._cvrp_step = addr("co_cvrp_step")
 
-    def tsp_decode_step(self, *args):
-        return self.mod.tsp_decode_step(self._tsp_decode_step, *args)
+        def bound(fn, entry):
+            return functools.partial(fn, ctypes.cast(getattr(lib, entry), ctypes.c_void_p).value)
 
-    def decode_step(self, *args):
-        return self.mod.decode_step(self._decode_step, *args)
-
-    def cvrp_step(self, *args):
-        return self.mod.cvrp_step(self._cvrp_step, *args)
+        self.tsp_decode_step = bound(mod.tsp_decode_step, "co_tsp_decode_step")
+        self.tsp_step_td = bound(mod.tsp_step_td, "co_tsp_decode_step")
+        self.decode_step = bound(mod.decode_step, "co_decode_step")
+        self.cvrp_step = bound(mod.cvrp_step, "co_cvrp_step")
 
 
 def torchstep():

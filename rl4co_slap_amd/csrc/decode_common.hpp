@@ -518,7 +518,8 @@ struct GreedyRow {
   }
 
   // CO_DECODE_CERTIFIED: after softmax_shift with the fast math (v[k] = z'_k - m', L' the
-  // fast log-sum-exp) and select (sel), is `sel` provably the exact path's greedy action?
+  // fast log-sum-exp) and select (sel), is `sel` provably the exact path's greedy action
+  // (as far as this lane's elements go)?
   // The exact action is the first index of max fl(fl(z_k - m) - L) (z: the clipped /
   // masked / scaled logits the exact path computes).  Certified when the fast runner-up
   // trails the selected value by more than
@@ -529,14 +530,13 @@ struct GreedyRow {
   //   + 2 ulp bound of L     (then fl(d_k - L) < fl(0 - L) for every k != sel: no rounding
   //                          tie with the maximum)
   // and L' is finite.  Non-finite rows (all masked, NaN / inf logits) are never certified.
+  // Evaluated per lane over the lane's own elements (no group reduction: the caller
+  // only needs whether any lane of the wave failed, one ballot): the lane is certified
+  // when each of its elements other than sel trails by more than delta (masked entries
+  // are -inf; a NaN fails the comparison).
   template <int OPT>
   __device__ __forceinline__ bool certify(float L, int sel, int c0, int N, float clip,
                                           float temp) const {
-    float ru = -__builtin_inff();
-#pragma unroll
-    for (int k = 0; k < EPL; ++k)
-      if (c0 + k < N && c0 + k != sel) ru = fmaxf(ru, v[k]);  // masked entries are -inf
-    ru = grp_max<RL>(ru);
     int e;
     frexpf(fabsf(L) + 1.f, &e);               // |L| + 1 < 2^e: ulp(L) <= 2^(e - 24)
     float delta = ldexpf(1.f, e - 22) + 1e-7f;  // 2 x (2 ulp), margin included
@@ -546,7 +546,10 @@ struct GreedyRow {
       const float ez = clip * 1.5e-6f + ldexpf(3.f, ec - 24);
       delta += 2.f * ((OPT & kOptTemp) ? ez / temp : ez);
     }
-    return __builtin_isfinite(L) && -ru > delta;  // ru NaN -> false
+    bool ok = __builtin_isfinite(L);
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) ok &= (c0 + k >= N) | (c0 + k == sel) | (v[k] < -delta);
+    return ok;
   }
 
   // greedy action of the row (valid on every lane of the group) and its logp

@@ -17,6 +17,7 @@
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "co_env.h"
 
@@ -59,111 +60,275 @@ PyObject* wrap_all(std::initializer_list<at::Tensor*> ts) {
   return out;
 }
 
-// the step's outputs: one storage, carved into the tensors (each a fresh, contiguous,
-// non-overlapping region, 256-byte aligned as the caching allocator's blocks are, so the
-// kernels' vector paths apply -- as separate allocations would be, at one allocator call)
+// Output memory.  Every output is a fresh, contiguous, non-overlapping region, 256-byte
+// aligned as the caching allocator's blocks are (so the kernels' vector paths apply), made
+// as a TensorImpl over a shared storage without a dispatcher call:
+// * the env state of a step (mask, i, first node, done, reward; CVRP used capacity,
+//   visited, current node, mask) shares one storage taken from a small per-device pool,
+//   reused only when no tensor refers to it any more (storage use count 1: the pool's);
+//   kernels queued on the same stream as every earlier user, as the caching allocator's
+//   own reuse is;
+// * the decoding strategy keeps every step's action and log-probability, so those come
+//   from a slab that serves several steps (freed when its last step's tensors go).
 constexpr int64_t kAlign = 256;
-struct Carve {
-  at::Tensor chunk;
-  int64_t off = 0;
-  at::Tensor take(at::IntArrayRef sizes, at::ScalarType dt) {
-    const int64_t es = (int64_t)c10::elementSize(dt);
-    off = (off + kAlign - 1) & ~(kAlign - 1);
-    int64_t n = 1;
-    for (auto s : sizes) n *= s;
-    auto t = at::empty({0}, chunk.options().dtype(dt));
-    t.set_(chunk.storage(), off / es, sizes);
-    off += n * es;
-    return t;
+
+inline int64_t up(int64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+at::Tensor view_of(const c10::Storage& st, at::ScalarType dt, int64_t off_bytes,
+                   at::IntArrayRef sizes) {
+  auto impl = c10::make_intrusive<c10::TensorImpl>(
+      c10::Storage(st), c10::DispatchKeySet(c10::DispatchKey::CUDA),
+      c10::scalarTypeToTypeMeta(dt));
+  impl->set_sizes_contiguous(sizes);
+  impl->set_storage_offset(off_bytes / (int64_t)c10::elementSize(dt));
+  return at::Tensor(std::move(impl));
+}
+
+c10::Storage new_storage(const c10::Device& dev, int64_t nbytes) {
+  return at::empty({nbytes}, at::TensorOptions().dtype(at::kByte).device(dev)).storage();
+}
+
+struct StatePool {
+  static constexpr int kPerKey = 4;
+  struct Entry {
+    c10::Device dev;
+    int64_t nbytes;
+    c10::Storage st;
+  };
+  std::vector<Entry> entries;
+  c10::Storage acquire(const c10::Device& dev, int64_t nbytes) {
+    int same = 0;
+    for (auto& e : entries) {
+      if (e.dev != dev || e.nbytes != nbytes) continue;
+      ++same;
+      if (e.st.use_count() == 1) return e.st;
+    }
+    c10::Storage st = new_storage(dev, nbytes);
+    if (same < kPerKey) entries.push_back(Entry{dev, nbytes, st});
+    return st;
   }
 };
 
-int64_t carve_bytes(std::initializer_list<int64_t> parts) {
-  int64_t s = 0;
-  for (auto p : parts) s = ((s + kAlign - 1) & ~(kAlign - 1)) + p;
-  return s;
-}
-
-// tsp_decode_step(fn, logits, mask, i, first_in, action_in, status, clip, temp, mode,
-//                 seed, offset, take) -> (act, logp, mask_out, i_out, first_out, done,
-//                 reward) | None
-// fn: address of co_tsp_decode_step; first_in / action_in: tensor or None.
-PyObject* tsp_decode_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
-  if (n != 13) {
-    PyErr_SetString(PyExc_TypeError, "tsp_decode_step: 13 arguments");
-    return nullptr;
+struct Slab {
+  static constexpr int64_t kSteps = 64;
+  c10::Device dev{c10::DeviceType::CPU};
+  c10::Storage st;
+  int64_t off = 0, cap = 0;
+  // a region of nbytes (a multiple of kAlign): offset into `st`
+  int64_t take(const c10::Device& d, int64_t nbytes) {
+    if (!st || d != dev || off + nbytes > cap) {
+      cap = nbytes * kSteps;
+      st = new_storage(d, cap);
+      dev = d;
+      off = 0;
+    }
+    const int64_t o = off;
+    off += nbytes;
+    return o;
   }
-  if (!is_tensor(a[1]) || !is_tensor(a[2]) || !is_tensor(a[3]) || !is_tensor(a[6]))
-    Py_RETURN_NONE;
-  const auto fn = fn_at<TspDecodeStep>(a[0]);
-  const at::Tensor& logits = THPVariable_Unpack(a[1]);
-  const at::Tensor& mask = THPVariable_Unpack(a[2]);
-  const at::Tensor& i = THPVariable_Unpack(a[3]);
-  const at::Tensor& status = THPVariable_Unpack(a[6]);
-  const bool has_first = is_tensor(a[4]), has_ain = is_tensor(a[5]);
-  const double clip = PyFloat_AsDouble(a[7]), temp = PyFloat_AsDouble(a[8]);
-  const long mode = PyLong_AsLong(a[9]);
-  const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[10]);
-  const uint64_t offset = PyLong_AsUnsignedLongLongMask(a[11]);
-  const long take = PyLong_AsLong(a[12]);
-  if (PyErr_Occurred()) return nullptr;
+};
+
+StatePool g_state;  // the GIL serialises every call into this module
+Slab g_slab;
+
+// carves one storage: take(bytes) returns the next aligned offset
+struct Carver {
+  int64_t off = 0;
+  int64_t take(int64_t nbytes) {
+    const int64_t o = off;
+    off += up(nbytes);
+    return o;
+  }
+};
+
+// The fused TSP decode step's operand checks, output memory and launch (shared by
+// tsp_decode_step and tsp_step_td).  Returns -1 when the operands do not fit (the caller's
+// Python path handles them), else the C ABI's status; out = act, logp, mask_out, i_out,
+// first_out, done, reward.
+int tsp_launch(TspDecodeStep fn, const at::Tensor& logits, const at::Tensor& mask,
+               const at::Tensor& i, const at::Tensor* first, const at::Tensor* ain,
+               const at::Tensor& status, double clip, double temp, long mode, uint64_t seed,
+               uint64_t offset, long take, at::Tensor (&out)[7]) {
   // the conditions envs/tsp.py:decode_and_step checks before its launch
   const c10::Device dev = mask.device();
   if (!dev.is_cuda() || logits.device() != dev || i.device() != dev || status.device() != dev ||
       logits.scalar_type() != at::kFloat || logits.dim() != 2 || logits.stride(1) != 1 ||
       mask.dim() != 2 || mask.scalar_type() != at::kBool || !mask.is_contiguous() ||
       i.scalar_type() != at::kLong || !i.is_contiguous() || status.scalar_type() != at::kInt)
-    Py_RETURN_NONE;
+    return -1;
   const int64_t b = mask.size(0), nl = mask.size(1);
-  if (logits.size(0) != b || logits.size(1) != nl || nl > 2048 || i.numel() != b)
-    Py_RETURN_NONE;
-  const at::Tensor* first = nullptr;
-  if (has_first && !take) {
-    first = &THPVariable_Unpack(a[4]);
-    if (first->device() != dev || first->scalar_type() != at::kLong || !first->is_contiguous() ||
-        first->numel() != b)
-      Py_RETURN_NONE;
-  } else if (!take) {
-    Py_RETURN_NONE;
+  if (logits.size(0) != b || logits.size(1) != nl || nl > 2048 || i.numel() != b) return -1;
+  if (!take && (!first || !fits(*first, dev, at::kLong, b))) return -1;
+  if (ain && !fits(*ain, dev, at::kLong, b)) return -1;
+  const int64_t kb = up(8 * b);
+  const int64_t ko = g_slab.take(dev, 2 * kb);
+  out[0] = view_of(g_slab.st, at::kLong, ko, {b});
+  out[1] = view_of(g_slab.st, at::kFloat, ko + kb, {b});
+  Carver c;
+  const int64_t om = c.take(b * nl), oi = c.take(8 * b), of = c.take(8 * b), od = c.take(b),
+                orw = c.take(b);
+  const c10::Storage st = g_state.acquire(dev, c.off);
+  out[2] = view_of(st, at::kBool, om, {b, nl});
+  out[3] = view_of(st, at::kLong, oi, i.sizes());
+  out[4] = view_of(st, at::kLong, of, {b});
+  out[5] = view_of(st, at::kBool, od, {b});
+  out[6] = view_of(st, at::kBool, orw, {b});
+  void* stream = current_stream(dev);
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = fn(b, nl, logits.const_data_ptr<float>(), logits.stride(0),
+          static_cast<const uint8_t*>(mask.const_data_ptr()), (float)clip, (float)temp, (int)mode,
+          ain ? ain->const_data_ptr<int64_t>() : nullptr, out[0].mutable_data_ptr<int64_t>(),
+          out[1].mutable_data_ptr<float>(), seed, offset,
+          static_cast<uint8_t*>(out[2].mutable_data_ptr()), i.const_data_ptr<int64_t>(),
+          out[3].mutable_data_ptr<int64_t>(), take ? nullptr : first->const_data_ptr<int64_t>(),
+          out[4].mutable_data_ptr<int64_t>(), (int)take,
+          static_cast<uint8_t*>(out[5].mutable_data_ptr()),
+          static_cast<uint8_t*>(out[6].mutable_data_ptr()), nullptr,
+          status.mutable_data_ptr<int32_t>(), stream);
+  Py_END_ALLOW_THREADS
+  return rc;
+}
+
+// tsp_decode_step(fn, logits, mask, i, first_in, action_in, status, clip, temp, mode,
+//                 seed, offset, take) -> (act, logp, mask_out, i_out, first_out, done,
+//                 reward) | None | error code
+// fn: address of co_tsp_decode_step; first_in / action_in: tensor or None.
+PyObject* tsp_decode_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 13) {
+    PyErr_SetString(PyExc_TypeError, "tsp_decode_step: 13 arguments");
+    return nullptr;
   }
-  const at::Tensor* ain = nullptr;
-  if (has_ain) {
-    ain = &THPVariable_Unpack(a[5]);
-    if (ain->device() != dev || ain->scalar_type() != at::kLong || !ain->is_contiguous() ||
-        ain->numel() != b)
-      Py_RETURN_NONE;
-  }
+  if (!is_tensor(a[1]) || !is_tensor(a[2]) || !is_tensor(a[3]) || !is_tensor(a[6]) ||
+      (a[4] != Py_None && !is_tensor(a[4])) || (a[5] != Py_None && !is_tensor(a[5])))
+    Py_RETURN_NONE;
+  const auto fn = fn_at<TspDecodeStep>(a[0]);
+  const double clip = PyFloat_AsDouble(a[7]), temp = PyFloat_AsDouble(a[8]);
+  const long mode = PyLong_AsLong(a[9]);
+  const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[10]);
+  const uint64_t offset = PyLong_AsUnsignedLongLongMask(a[11]);
+  const long take = PyLong_AsLong(a[12]);
+  if (PyErr_Occurred()) return nullptr;
   try {
-    // the decoding strategy keeps every step's action and log-probability, the env only
-    // the latest state: two chunks, so a kept action does not pin a stale mask
-    Carve k, c;
-    k.chunk = at::empty({carve_bytes({8 * b, 4 * b})}, mask.options().dtype(at::kByte));
-    c.chunk = at::empty({carve_bytes({b * nl, 8 * b, 8 * b, b, b})},
-                        mask.options().dtype(at::kByte));
-    at::Tensor act = k.take({b}, at::kLong), logp = k.take({b}, at::kFloat);
-    at::Tensor mask_out = c.take({b, nl}, at::kBool), i_out = c.take(i.sizes(), at::kLong);
-    at::Tensor first_out = c.take({b}, at::kLong), done = c.take({b}, at::kBool);
-    at::Tensor reward = c.take({b}, at::kBool);
-    void* stream = current_stream(dev);
-    int rc;
-    Py_BEGIN_ALLOW_THREADS
-    rc = fn(b, nl, logits.const_data_ptr<float>(), logits.stride(0),
-            static_cast<const uint8_t*>(mask.const_data_ptr()), (float)clip, (float)temp,
-            (int)mode, ain ? ain->const_data_ptr<int64_t>() : nullptr,
-            act.mutable_data_ptr<int64_t>(), logp.mutable_data_ptr<float>(), seed, offset,
-            static_cast<uint8_t*>(mask_out.mutable_data_ptr()), i.const_data_ptr<int64_t>(),
-            i_out.mutable_data_ptr<int64_t>(), first ? first->const_data_ptr<int64_t>() : nullptr,
-            first_out.mutable_data_ptr<int64_t>(), (int)take,
-            static_cast<uint8_t*>(done.mutable_data_ptr()),
-            static_cast<uint8_t*>(reward.mutable_data_ptr()), nullptr,
-            status.mutable_data_ptr<int32_t>(), stream);
-    Py_END_ALLOW_THREADS
+    at::Tensor out[7];
+    const int rc = tsp_launch(fn, THPVariable_Unpack(a[1]), THPVariable_Unpack(a[2]),
+                              THPVariable_Unpack(a[3]),
+                              is_tensor(a[4]) ? &THPVariable_Unpack(a[4]) : nullptr,
+                              is_tensor(a[5]) ? &THPVariable_Unpack(a[5]) : nullptr,
+                              THPVariable_Unpack(a[6]), clip, temp, mode, seed, offset, take, out);
+    if (rc < 0) Py_RETURN_NONE;
     if (rc != CO_OK) return PyLong_FromLong(rc);  // the caller raises _native's error
-    return wrap_all({&act, &logp, &mask_out, &i_out, &first_out, &done, &reward});
+    return wrap_all({&out[0], &out[1], &out[2], &out[3], &out[4], &out[5], &out[6]});
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());
     return nullptr;
   }
+}
+
+// ---- host-side knowledge on state tensors (envs/base.py) ---------------------------
+// A record (version, value) in a tensor's attribute: valid while the tensor's version
+// counter is unchanged (nobody modified it in place since the env produced it).
+PyObject* g_attr_i = nullptr;  // "_co_i": the value every entry of an `i` tensor holds
+
+// the record's value, or -1 (absent / stale)
+long long known(PyObject* t, PyObject* attr) {
+  PyObject* rec = nullptr;
+  if (_PyObject_LookupAttr(t, attr, &rec) <= 0) {
+    PyErr_Clear();
+    return -1;
+  }
+  long long v = -1;
+  if (PyTuple_Check(rec) && PyTuple_GET_SIZE(rec) == 2) {
+    const long long ver = PyLong_AsLongLong(PyTuple_GET_ITEM(rec, 0));
+    if (ver == (long long)THPVariable_Unpack(t)._version())
+      v = PyLong_AsLongLong(PyTuple_GET_ITEM(rec, 1));
+    if (PyErr_Occurred()) {
+      PyErr_Clear();
+      v = -1;
+    }
+  }
+  Py_DECREF(rec);
+  return v;
+}
+
+int remember(PyObject* t, PyObject* attr, long long value) {
+  PyObject* rec = Py_BuildValue("(LL)", (long long)THPVariable_Unpack(t)._version(), value);
+  if (!rec) return -1;
+  const int r = PyObject_SetAttr(t, attr, rec);
+  Py_DECREF(rec);
+  return r;
+}
+
+// tsp_step_td(fn, lb_attr, td, logits, mode, temp, clip, action_in, seed, offset, status,
+//             key) -> (action, logp) | None | error code
+// TSPEnv.decode_and_step on a dict-backed TensorDict: reads action_mask / i / first_node,
+// checks the env's knowledge of i (the batch-wide first-node test), launches, records
+// i + 1 and the done lower bound (attribute lb_attr) on the new state tensors and stores
+// the new state in the td -- what envs/tsp.py does around tsp_decode_step, without the
+// Python frames.  (fn, lb_attr) lead so that a functools.partial binds them.
+PyObject* tsp_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 12) {
+    PyErr_SetString(PyExc_TypeError, "tsp_step_td: 12 arguments");
+    return nullptr;
+  }
+  PyObject* td = a[2];
+  PyObject* lb_attr = a[1];
+  PyObject* key = a[11];
+  PyObject* ain_o = a[7];
+  if (!PyDict_Check(td) || !is_tensor(a[3]) || !is_tensor(a[10]) ||
+      (ain_o != Py_None && !is_tensor(ain_o)) || !PyUnicode_Check(key) ||
+      !PyUnicode_Check(lb_attr))
+    Py_RETURN_NONE;
+  PyObject* mask_o = PyDict_GetItemString(td, "action_mask");  // borrowed
+  PyObject* i_o = PyDict_GetItemString(td, "i");
+  if (!mask_o || !i_o || !is_tensor(mask_o) || !is_tensor(i_o)) Py_RETURN_NONE;
+  const long long k = known(i_o, g_attr_i);
+  if (k < 0) Py_RETURN_NONE;
+  const long take = k == 0 ? 1 : 0;
+  PyObject* first_o = take ? nullptr : PyDict_GetItemString(td, "first_node");
+  if (!take && (!first_o || !is_tensor(first_o))) Py_RETURN_NONE;
+  const auto fn = fn_at<TspDecodeStep>(a[0]);
+  const long mode = PyLong_AsLong(a[4]);
+  const double temp = PyFloat_AsDouble(a[5]), clip = PyFloat_AsDouble(a[6]);
+  const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[8]);
+  const uint64_t offset = PyLong_AsUnsignedLongLongMask(a[9]);
+  if (PyErr_Occurred()) return nullptr;
+  at::Tensor out[7];
+  try {
+    const int rc = tsp_launch(fn, THPVariable_Unpack(a[3]), THPVariable_Unpack(mask_o),
+                              THPVariable_Unpack(i_o),
+                              first_o ? &THPVariable_Unpack(first_o) : nullptr,
+                              ain_o != Py_None ? &THPVariable_Unpack(ain_o) : nullptr,
+                              THPVariable_Unpack(a[10]), clip, temp, mode, seed, offset, take,
+                              out);
+    if (rc < 0) Py_RETURN_NONE;
+    if (rc != CO_OK) return PyLong_FromLong(rc);
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+  const long long lb = known(mask_o, lb_attr);
+  PyObject* o[7];
+  for (int j = 0; j < 7; ++j) {
+    o[j] = THPVariable_Wrap(std::move(out[j]));
+    if (!o[j]) {
+      for (int q = 0; q < j; ++q) Py_DECREF(o[q]);
+      return nullptr;
+    }
+  }
+  PyObject* sel = ain_o != Py_None ? ain_o : o[0];
+  int err = remember(o[3], g_attr_i, k + 1);
+  if (!err && lb >= 0) err = remember(o[2], lb_attr, lb > 0 ? lb - 1 : 0);
+  if (!err) err = PyDict_SetItem(td, key, sel);
+  if (!err) err = PyDict_SetItemString(td, "first_node", o[4]);
+  if (!err) err = PyDict_SetItemString(td, "current_node", sel);
+  if (!err) err = PyDict_SetItemString(td, "i", o[3]);
+  if (!err) err = PyDict_SetItemString(td, "action_mask", o[2]);
+  if (!err) err = PyDict_SetItemString(td, "reward", o[6]);
+  if (!err) err = PyDict_SetItemString(td, "done", o[5]);
+  PyObject* res = err ? nullptr : PyTuple_Pack(2, sel, o[1]);
+  for (int j = 0; j < 7; ++j) Py_DECREF(o[j]);
+  return res;
 }
 
 // decode_step(fn, logits, mask, action_in, status, clip, temp, mode, seed, offset, full)
@@ -208,9 +373,10 @@ PyObject* decode_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
     Py_RETURN_NONE;
   }
   try {
-    Carve k;
-    k.chunk = at::empty({carve_bytes({8 * b, 4 * b})}, logits.options().dtype(at::kByte));
-    at::Tensor act = k.take({b}, at::kLong), logp = k.take({b}, at::kFloat), full;
+    const int64_t kb = up(8 * b);
+    const int64_t ko = g_slab.take(dev, 2 * kb);
+    at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
+    at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b}), full;
     if (want_full) full = at::empty({b, nl}, logits.options());
     void* stream = current_stream(dev);
     int rc;
@@ -255,13 +421,16 @@ PyObject* cvrp_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
       !fits(visited, dev, at::kByte, b * (nl + 1)))
     Py_RETURN_NONE;
   try {
-    Carve c;
-    c.chunk = at::empty({carve_bytes({4 * b, b * (nl + 1), 8 * b, b, b, b * (nl + 1)})},
-                        demand.options().dtype(at::kByte));
-    at::Tensor used_out = c.take(used.sizes(), at::kFloat);
-    at::Tensor visited_out = c.take(visited.sizes(), at::kByte);
-    at::Tensor cur = c.take({b, 1}, at::kLong), done = c.take({b}, at::kBool);
-    at::Tensor reward = c.take({b}, at::kBool), mask = c.take({b, nl + 1}, at::kBool);
+    Carver c;
+    const int64_t ou = c.take(4 * b), ov = c.take(b * (nl + 1)), oc = c.take(8 * b),
+                  od = c.take(b), orw = c.take(b), om = c.take(b * (nl + 1));
+    const c10::Storage st = g_state.acquire(dev, c.off);
+    at::Tensor used_out = view_of(st, at::kFloat, ou, used.sizes());
+    at::Tensor visited_out = view_of(st, at::kByte, ov, visited.sizes());
+    at::Tensor cur = view_of(st, at::kLong, oc, {b, 1});
+    at::Tensor done = view_of(st, at::kBool, od, {b});
+    at::Tensor reward = view_of(st, at::kBool, orw, {b});
+    at::Tensor mask = view_of(st, at::kBool, om, {b, nl + 1});
     void* stream = current_stream(dev);
     int rc;
     Py_BEGIN_ALLOW_THREADS
@@ -282,6 +451,8 @@ PyObject* cvrp_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
 }
 
 PyMethodDef methods[] = {
+    {"tsp_step_td", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(tsp_step_td)),
+     METH_FASTCALL, "TSPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
     {"decode_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(decode_step)),
      METH_FASTCALL, "decode step: outputs allocated and launched in one call"},
     {"cvrp_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(cvrp_step)),
@@ -296,4 +467,8 @@ PyModuleDef module = {PyModuleDef_HEAD_INIT, "_co_torchstep",
 
 }  // namespace
 
-PyMODINIT_FUNC PyInit__co_torchstep(void) { return PyModule_Create(&module); }
+PyMODINIT_FUNC PyInit__co_torchstep(void) {
+  g_attr_i = PyUnicode_InternFromString("_co_i");
+  if (!g_attr_i) return nullptr;
+  return PyModule_Create(&module);
+}

@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import abc
 import os
-import weakref
 from typing import Iterable, Optional
 
 import torch
@@ -68,12 +67,11 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         if seed is None:
             seed = torch.empty((), dtype=torch.int64).random_().item()
         self.set_seed(seed)
-        # host-side knowledge of td["i"] tensors this env produced:
-        # id(tensor) -> (weakref, version, uniform value)
-        self._i_known = {}
-        # lower bounds on the steps before `done` can be all true, keyed by the state
-        # tensor the bound is about (same weakref/version bookkeeping)
-        self._lb_known = {}
+        # host-side knowledge about state tensors the env produced is kept ON those tensors
+        # as (version, value) attributes, valid while the tensor's version counter is
+        # unchanged: "_co_i" = the value every entry of a td["i"] holds, and the lower bound
+        # on the steps before `done` can be all true under this env's own attribute name
+        self._lb_attr = "_co_lb_" + self.name
         # the step functions' fresh outputs (utils/pool.py); CO_NO_POOL=1: torch.empty
         self._pool = None if os.environ.get("CO_NO_POOL") else OutputPool()
 
@@ -204,16 +202,18 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
                 raise exc(msg)
 
     # -- i-tracking for the batch-wide `i.all() == 0` test ------------------------
-    def _remember_i(self, t: torch.Tensor, value: int):
-        if len(self._i_known) > 64:  # drop entries whose tensors are gone
-            self._i_known = {k: v for k, v in self._i_known.items() if v[0]() is not None}
-        self._i_known[id(t)] = (weakref.ref(t), t._version, value)
+    # (the record lives on the tensor: it dies with it, and an in-place change bumps the
+    # version; csrc/pycall/co_torchstep.cpp reads and writes the same records)
+    @staticmethod
+    def _remember_i(t: torch.Tensor, value: int):
+        t._co_i = (t._version, value)
 
-    def _known_i(self, t: torch.Tensor):
-        rec = self._i_known.get(id(t))
-        if rec is None or rec[0]() is not t or rec[1] != t._version:
+    @staticmethod
+    def _known_i(t: torch.Tensor):
+        rec = getattr(t, "_co_i", None)
+        if rec is None or rec[0] != t._version:
             return None
-        return rec[2]
+        return rec[1]
 
     # -- step outputs -------------------------------------------------------------
     def _out(self, shape, dtype, device, stream):
@@ -223,23 +223,22 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         if self._pool is None:
             return torch.empty(shape, dtype=dtype, device=device)
         t = self._pool.empty(shape, dtype, device, stream)
-        self._i_known.pop(id(t), None)
-        self._lb_known.pop(id(t), None)
+        d = t.__dict__
+        d.pop("_co_i", None)
+        d.pop(self._lb_attr, None)
         return t
 
     # -- done-poll lower bounds ---------------------------------------------------
     def _remember_lb(self, t: torch.Tensor, steps: int):
-        if len(self._lb_known) > 64:
-            self._lb_known = {k: v for k, v in self._lb_known.items() if v[0]() is not None}
-        self._lb_known[id(t)] = (weakref.ref(t), t._version, max(int(steps), 0))
+        setattr(t, self._lb_attr, (t._version, max(int(steps), 0)))
 
     def _known_lb(self, t) -> Optional[int]:
         if not isinstance(t, torch.Tensor):
             return None
-        rec = self._lb_known.get(id(t))
-        if rec is None or rec[0]() is not t or rec[1] != t._version:
+        rec = getattr(t, self._lb_attr, None)
+        if rec is None or rec[0] != t._version:
             return None
-        return rec[2]
+        return rec[1]
 
     def min_steps_to_done(self, td) -> int:
         """A host-side lower bound on the env steps still needed before every instance

@@ -7,7 +7,7 @@ import torch
 from torch.distributions import Uniform
 
 from .. import _native as nat
-from ..td import TensorDict
+from ..td import TensorDict, set_many
 from .base import RL4COEnvBase
 from .common import Generator, device_uniform, get_sampler
 
@@ -145,8 +145,8 @@ class CVRPEnv(RL4COEnvBase):
         lb = self._known_lb(td["visited"])
         if lb is not None:  # a step marks at most one more node visited
             self._remember_lb(visited_out, lb - 1)
-        td.update({"current_node": cur, "used_capacity": used_out, "visited": visited_out,
-                   "reward": reward, "done": done, "action_mask": mask})
+        set_many(td, {"current_node": cur, "used_capacity": used_out, "visited": visited_out,
+                      "reward": reward, "done": done, "action_mask": mask})
         return td
 
     def min_steps_to_done(self, td) -> int:

@@ -7,7 +7,7 @@ import torch
 from torch.distributions import Uniform
 
 from .. import _native as nat
-from ..td import RepeatedRows, TensorDict
+from ..td import RepeatedRows, TensorDict, set_many
 from .base import RL4COEnvBase
 from .common import Generator, device_uniform, get_sampler
 
@@ -108,12 +108,34 @@ class TSPEnv(RL4COEnvBase):
         and aliasing (``current_node`` is the action tensor) as the two calls.  Returns
         ``(action, logp)``, or None when it does not apply (CPU tensors, unknown ``i``
         provenance for the batch-wide first-node test, non-f32 logits)."""
-        mask, i = td["action_mask"], td["i"]
-        if logits.device.type != "cuda" or mask.device != logits.device:
+        ts = nat.torchstep()
+        if ts is not None:  # the whole step, bookkeeping included, in one native call
+            r = ts.tsp_step_td(self._lb_attr, td, logits, mode, temperature, tanh_clipping,
+                               action_in, seed, offset, status, key)
+            if r is not None:
+                if type(r) is int:
+                    nat.check_rc("co_tsp_decode_step", r)
+                return r
+        return self._decode_and_step_py(td, logits, mode, temperature, tanh_clipping,
+                                        action_in, seed, offset, status, key)
+
+    def native_decode_and_step(self):
+        """``decode_and_step``'s native call for a decoding strategy's loop: ``f(td,
+        logits, mode, temperature, tanh_clipping, action_in, seed, offset, status, key)``
+        returning ``(action, logp)``, an error code, or None (then call
+        ``decode_and_step``); None when the step glue is unavailable."""
+        ts = nat.torchstep()
+        if ts is None:
             return None
+        import functools
+
+        return functools.partial(ts.tsp_step_td, self._lb_attr)
+
+    def _decode_and_step_py(self, td, logits, mode, temperature, tanh_clipping, action_in,
+                            seed, offset, status, key):
+        mask, i = td["action_mask"], td["i"]
         known = self._known_i(i)
-        if known is None or logits.dtype != torch.float32 or logits.dim() != 2 \
-                or logits.stride(-1) != 1:
+        if known is None:
             return None
         first_in = td.get("first_node", None)
         take = 1 if known == 0 else 0
@@ -128,42 +150,45 @@ class TSPEnv(RL4COEnvBase):
                 if type(r) is int:
                     nat.check_rc("co_tsp_decode_step", r)
                 act, logp, mask_out, i_out, first_out, done, reward = r
-                return self._after_decode_step(td, key, action_in, act, logp, mask_out, i_out,
-                                               first_out, done, reward, known)
+                return self._after_decode_step(td, key, action_in, act, logp, mask, mask_out,
+                                               i_out, first_out, done, reward, known)
+        if logits.device.type != "cuda" or mask.device != logits.device:
+            return None
+        if logits.dtype != torch.float32 or logits.dim() != 2 or logits.stride(-1) != 1:
+            return None
         b, n = mask.shape
         if logits.shape != (b, n) or n > 2048:  # long rows: co_decode_step's row kernel
             return None
         dev = mask.device
-        mask, i = mask.contiguous(), i.contiguous()
+        m, i = mask.contiguous(), i.contiguous()
         first_in = first_in.contiguous() if (first_in is not None and not take) else None
         ain = action_in.long().contiguous() if action_in is not None else None
-        s = nat.stream_of(mask)
+        s = nat.stream_of(m)
         # the decoding strategy keeps every action and log-probability: never pooled
         act = torch.empty(b, dtype=torch.int64, device=dev)
         logp = torch.empty(b, dtype=torch.float32, device=dev)
-        mask_out = self._out(mask.shape, mask.dtype, dev, s)
+        mask_out = self._out(m.shape, m.dtype, dev, s)
         i_out = self._out(i.shape, i.dtype, dev, s)
         first_out = self._out((b,), torch.int64, dev, s)
         done = self._out((b,), torch.bool, dev, s)
         reward = self._out((b,), torch.bool, dev, s)
-        nat.call("co_tsp_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(mask),
+        nat.call("co_tsp_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(m),
                  float(tanh_clipping), float(temperature), mode, nat.ptr(ain), nat.ptr(act),
                  nat.ptr(logp), seed, offset, nat.ptr(mask_out), nat.ptr(i), nat.ptr(i_out),
                  nat.ptr(first_in), nat.ptr(first_out), take, nat.ptr(done), nat.ptr(reward),
                  None, nat.ptr(status), s)
-        return self._after_decode_step(td, key, action_in, act, logp, mask_out, i_out,
+        return self._after_decode_step(td, key, action_in, act, logp, mask, mask_out, i_out,
                                        first_out, done, reward, known)
 
-    def _after_decode_step(self, td, key, action_in, act, logp, mask_out, i_out, first_out,
-                           done, reward, known):
+    def _after_decode_step(self, td, key, action_in, act, logp, mask, mask_out, i_out,
+                           first_out, done, reward, known):
         sel = action_in if action_in is not None else act
         self._remember_i(i_out, known + 1)
-        lb = self._known_lb(td["action_mask"])
+        lb = self._known_lb(mask)
         if lb is not None:
             self._remember_lb(mask_out, lb - 1)
-        td.set(key, sel)
-        td.update({"first_node": first_out, "current_node": sel, "i": i_out,
-                   "action_mask": mask_out, "reward": reward, "done": done})
+        set_many(td, {key: sel, "first_node": first_out, "current_node": sel, "i": i_out,
+                      "action_mask": mask_out, "reward": reward, "done": done})
         return sel, logp
 
     def _get_reward(self, td, actions, check: bool = False) -> torch.Tensor:

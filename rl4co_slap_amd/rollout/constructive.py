@@ -28,6 +28,22 @@ from ..utils.ops import calculate_entropy
 log = logging.getLogger(__name__)
 
 
+def _direct_call(m):
+    """``m.forward`` when calling the module would go straight to it (nn.Module's own fast
+    path: no hooks of any kind, not compiled, not tracing), so the decode loop skips the call wrapper's
+    per-step checks; else ``m`` itself.  Decided once per ``forward``."""
+    from torch.nn.modules import module as M
+
+    if (not isinstance(m, nn.Module) or getattr(m, "_compiled_call_impl", None) is not None
+            or torch._C._get_tracing_state()):
+        return m
+    if (m._backward_hooks or m._backward_pre_hooks or m._forward_hooks or m._forward_pre_hooks
+            or M._global_backward_pre_hooks or M._global_backward_hooks
+            or M._global_forward_hooks or M._global_forward_pre_hooks):
+        return m
+    return m.forward
+
+
 class NoEncoder(nn.Module):
     """``constructive/base.py:36-40``: no encoder, hidden = initial embeddings = None."""
 
@@ -112,8 +128,9 @@ class ConstructivePolicy(nn.Module):
         if hook is not None:
             td, env, hidden = hook(td, env, hidden, num_starts)
         step = 0
+        decode = _direct_call(self.decoder)
         while step < lb or not td["done"].all():
-            logits, mask = self.decoder(td, hidden, num_starts)
+            logits, mask = decode(td, hidden, num_starts)
             act = actions[..., step] if actions is not None else None
             # decode + env step as one launch where the env provides it (TSP), else both
             nxt = strategy.step_env_fused(logits, mask, td, env, action=act)

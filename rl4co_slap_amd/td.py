@@ -191,3 +191,13 @@ except ImportError:  # the stand-in
         def __repr__(self):
             fields = ", ".join(f"{k}: {tuple(v.shape)}" for k, v in dict.items(self))
             return f"TensorDict({{{fields}}}, batch_size={tuple(self.batch_size)}, device={self.device})"
+
+
+def set_many(td, entries: dict):
+    """``td.update(entries)`` for values already on the device of ``td``'s own tensors (a
+    step's outputs): the stand-in stores them without re-checking each value's device."""
+    if not HAVE_TENSORDICT and type(td) is TensorDict:
+        dict.update(td, entries)
+    else:
+        td.update(entries)
+    return td

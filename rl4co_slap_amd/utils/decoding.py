@@ -170,6 +170,7 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         self.actions, self.logprobs = [], []
         self._status = None
         self._step_idx = 0
+        self._fused = None  # (env, its decode_and_step or None, mode, mode word)
 
     def pre_decoder_hook(self, td, env, action=None):
         """``decoding.py:265-313``."""
@@ -260,20 +261,40 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         observe the difference: the env's own ``step``, the mask the env holds, no full
         log-probabilities / top-k / top-p.  Same outputs, same RNG use; returns the next
         td, or None when the fused path does not apply (the caller runs both steps)."""
-        fused = getattr(env, "decode_and_step", None)
-        if (fused is None or _NO_FUSED or self.store_all_logp or self.improvement_method_mode
-                or self.top_k > 0 or 0.0 < self.top_p < 1.0 or not self.mask_logits
-                or getattr(env, "_torchrl_mode", False) or mask is not td.get("action_mask")):
+        # the strategy-side conditions, decided once per env (the settings do not change
+        # inside a decode loop)
+        cached = self._fused
+        if cached is None or cached[0] is not env:
+            fused = getattr(env, "decode_and_step", None)
+            mode = self._mode()
+            if (fused is None or _NO_FUSED or self.store_all_logp or self.improvement_method_mode
+                    or self.top_k > 0 or 0.0 < self.top_p < 1.0 or not self.mask_logits
+                    or mode not in _MODES):
+                fused = None
+            # the env's native form of the same call (TSPEnv: csrc/pycall), tried first
+            native = getattr(env, "native_decode_and_step", None)
+            native = native() if (native is not None and fused is not None) else None
+            cached = self._fused = (env, fused, native, mode,
+                                    _MODES.get(mode, 0) | self._math_flags)
+        _, fused, native, mode, mword = cached
+        if fused is None or getattr(env, "_torchrl_mode", False):
             return None
-        mode = self._mode()
-        if mode not in _MODES:
+        held = dict.get(td, "action_mask") if type(td) is TensorDict else td.get("action_mask")
+        if mask is not held:
             return None
         if self._status is None:
             self._status = nat.scratch_status(logits.device)
         seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
-        out = fused(td, logits, _MODES[mode] | self._math_flags, self.temperature, self.tanh_clipping,
-                    action if mode == "evaluate" else None, seed, self._step_idx, self._status,
-                    self.key)
+        ain = action if mode == "evaluate" else None
+        out = None
+        if native is not None:
+            out = native(td, logits, mword, self.temperature, self.tanh_clipping, ain, seed,
+                         self._step_idx, self._status, self.key)
+            if type(out) is int:
+                nat.check_rc("decode_and_step", out)
+        if out is None:
+            out = fused(td, logits, mword, self.temperature, self.tanh_clipping, ain, seed,
+                        self._step_idx, self._status, self.key)
         if out is None:
             if mode == "sampling":  # the seed draw above stands in for decode_step's
                 self._seed_carry = seed

@@ -124,3 +124,35 @@ def test_glue_steps_aside(dev):
     assert len(set(ptrs)) == len(ptrs) and all(p % 256 == 0 for p in ptrs)
     torch.cuda.synchronize()
     assert int(st.item()) == 0
+
+
+def test_stale_records_fall_back(dev, python_path):
+    """A decoder that touches td["i"] / td["action_mask"] in place (version bump) voids the
+    host-side records on them: the native step steps aside, the loop takes the two-launch
+    path with the device-side first-node test and polls `done` -- same results as the
+    Python path."""
+    b, n = 33, 12
+    locs = torch.rand(b, n, 2, generator=torch.Generator().manual_seed(21))
+    tab = torch.randn(n + 2, b, n, generator=torch.Generator().manual_seed(22)).to(dev)
+
+    def run():
+        env = TSPEnv(generator_params=dict(num_loc=n), device=dev)
+        td = env.reset(TensorDict({"locs": locs.to(dev)}, [b]))
+        it = iter(range(10 ** 6))
+
+        def fn(t):
+            k = next(it)
+            if k in (0, 4):
+                t["i"].add_(0)
+            if k == 6:
+                t["action_mask"].mul_(True)
+            return tab[k]
+
+        pol = ConstructivePolicy(None, LogitsDecoder(fn), env_name="tsp")
+        return pol(td, env, phase="test", decode_type="greedy", return_actions=True)
+
+    glue = run()
+    with python_path():
+        ref = run()
+    _same(glue, ref)
+    assert glue["actions"].shape == (b, n)
