@@ -241,6 +241,29 @@ __device__ __forceinline__ void stage_bytes_lds(const unsigned char* __restrict_
   __syncthreads();
 }
 
+// The wave copies `nbytes` (16-byte aligned source and destination) global -> LDS with
+// LDS-DMA, 1 KiB per instruction; the caller waits (vmcnt) before reading.
+__device__ __forceinline__ void wave_dma(const unsigned char* __restrict__ src, int nbytes,
+                                         unsigned char* dst) {
+  const int lane = lane_id(), n16 = nbytes & ~15;
+  for (int base = 0; base < n16; base += 1024) {
+    if (base + lane * 16 < n16)
+      __builtin_amdgcn_global_load_lds((const void*)(src + base + lane * 16),
+                                       (lds_void*)(dst + base), 16, 0, 0);
+  }
+  if (lane < ((nbytes - n16) >> 2))  // a tail of whole dwords (< 16 B): plain loads
+    reinterpret_cast<uint32_t*>(dst + n16)[lane] = reinterpret_cast<const uint32_t*>(src + n16)[lane];
+}
+
+// After wave_dma: drain the wave's loads and make its LDS writes (DMA and the tail's plain
+// stores) visible to all of its lanes; no workgroup barrier.
+__device__ __forceinline__ void wave_dma_wait() {
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Zero a device int32 (flags / counters).  A kernel, not hipMemsetAsync: memset nodes
 // captured into HIP graphs were observed on MI355X to replay with a wrong fill byte
 // (0x10101010 after a 4-byte memset to 0), which corrupted counters in replays.

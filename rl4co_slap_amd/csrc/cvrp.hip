@@ -123,6 +123,9 @@ __global__ __launch_bounds__(256) void cvrp_step_kernel(
 // depot byte of each row is patched into its chunk after the barrier, so every byte of
 // the mask tile is written once by a 16-B store.  `not_done` (optional) receives one
 // atomicAdd per workgroup: the number of its rows that are not done.
+#ifndef CO_CVRP_QUAD
+#define CO_CVRP_QUAD 1  // co_cvrp_step takes the wave-per-quad kernel (below) when it can
+#endif
 #ifndef CO_CVRP_ROWS
 #define CO_CVRP_ROWS 64
 #endif
@@ -314,6 +317,147 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
     if (not_done) {
       const int left = __popcll(__ballot(!dn));
       if (tid == 0 && left) atomicAdd(not_done, left);
+    }
+  }
+}
+
+// Quad step (cvrp/env.py:73-149, the env step the tile kernel above also implements): one
+// wave owns 4 consecutive rows (a "quad"), 16 lanes per row.  The quad's [4, N] demand rows
+// are one contiguous 16N-byte block, staged into the wave's LDS slice by LDS-DMA; the
+// visited / action_mask rows (N+1 bytes, not 4-byte aligned) are read and written in place
+// as the aligned dwords that cover the row: lane sl of a row's group owns dwords
+// k = sl + 16j of it, byte e of dword k is column 4k + e - s (s: the row's first byte
+// within its first dword).  So every row-uniform value (action, used / vehicle capacity,
+// the row sums) is group-uniform, the per-dword work is word-wide (SWAR) except the f32
+// capacity test `demand + used > capacity` per byte, and the row reductions are 16-lane
+// DPP / ballot operations.  Interior dwords are stored whole; the row's first and last
+// dword, shared with the neighbouring rows, by byte stores of the row's own bytes.  No
+// workgroup barrier on the data path; `not_done` (optional): one atomic per workgroup.
+template <int U, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void cvrp_step_quad_kernel(
+    int64_t B, int N, const int64_t* __restrict__ action, const float* __restrict__ demand,
+    const float* __restrict__ used_in, float* __restrict__ used_out,
+    const float* __restrict__ vcap, const uint8_t* vis_in, uint8_t* vis_out,
+    int64_t* __restrict__ cur_out, uint8_t* __restrict__ done, uint8_t* __restrict__ reward,
+    uint8_t* __restrict__ mask, int32_t* status, int32_t* not_done) {
+  extern __shared__ __attribute__((aligned(16))) float s_quad[];  // per wave: 4 + 4N + 4 floats
+  __shared__ int s_left[WAVES];
+  const int lane = lane_id(), w = threadIdx.x >> 6, sl = lane & 15, grp = lane >> 4;
+  const int NC = N + 1;
+  float* const sd = s_quad + w * (8 + 4 * N) + 4;
+  const int64_t row0 = ((int64_t)blockIdx.x * WAVES + w) * 4;
+  int left = 0;
+  if (row0 < B) {
+    const int rows = (int)(B - row0 < 4 ? B - row0 : 4);
+    const bool valid = grp < rows;
+    const int64_t b = valid ? row0 + grp : row0;
+    // every global load before the one wait: the row scalars (group-uniform addresses)
+    const int64_t a_raw = action[b];
+    const float uin = used_in[b], cap = vcap[b];
+    const int64_t byte0 = b * NC;
+    const int s = (int)(byte0 & 3);
+    const int ndw = (s + NC + 3) >> 2;  // dwords covering the row
+    const uint32_t* vrow = reinterpret_cast<const uint32_t*>(vis_in) + (byte0 >> 2);
+    uint32_t v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int k = sl + 16 * j;
+      v[j] = 0u;
+      if (valid && k < ndw) {
+        if (b == B - 1 && k == ndw - 1 && ((byte0 + NC) & 3)) {  // the buffer's last bytes
+#pragma unroll
+          for (int e = 0; e < 3; ++e)
+            if (e < ((byte0 + NC) & 3)) v[j] |= (uint32_t)vis_in[byte0 - s + 4 * k + e] << (8 * e);
+        } else {
+          v[j] = vrow[k];
+        }
+      }
+    }
+    wave_dma(reinterpret_cast<const unsigned char*>(demand + row0 * N), rows * N * 4,
+             reinterpret_cast<unsigned char*>(sd));
+    wave_dma_wait();
+    // cvrp/env.py:79-85
+    const bool bad = a_raw < 0 || a_raw > N;
+    if (valid && bad && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
+    const float* drow = sd + grp * N;
+    int64_t di = a_raw - 1;
+    di = di < 0 ? 0 : (di > N - 1 ? N - 1 : di);
+    const float u = (uin + drow[di]) * ((a_raw != 0) ? 1.0f : 0.0f);
+    const int a = bad ? -1 : (int)a_raw;
+    uint32_t m[U];
+    uint32_t cnt = 0u;
+    bool feas = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int k = sl + 16 * j;
+      const bool live = valid && k < ndw;
+      const int cb = live ? 4 * k - s : 0;  // column of byte 0 (dead slots: dword 0's)
+      // the row's own bytes [lo, hi) of this dword; the depot byte (column 0) at -cb
+      const int lo = cb < 0 ? -cb : 0;
+      const int hi = NC - cb < 4 ? NC - cb : 4;
+      const uint32_t own = !live ? 0u
+                           : ((hi >= 4 ? 0xffffffffu : (1u << (8 * hi)) - 1u) &
+                              ~((1u << (8 * lo)) - 1u));
+      const uint32_t cust = cb <= 0 ? own & ~(0xffu << (8 * lo)) : own;  // depot excluded
+      uint32_t x = v[j];
+      const int ea = a - cb;  // the action's byte, if in this dword
+      if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
+      v[j] = x;
+      // demand of byte e: drow[cb + e - 1] (the slice's pad covers cb - 1 >= -4 and N + 2)
+      const float* dp = drow + (cb - 1);
+      uint32_t over = 0u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) over |= (dp[e] + u > cap) ? (0x80u << (8 * e)) : 0u;
+      const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+      const uint32_t mk = ((~(nz | over) & 0x80808080u) >> 7) & cust;
+      cnt = __builtin_amdgcn_sad_u8(x & own, 0u, cnt);
+      feas |= mk != 0u;
+      m[j] = mk;
+    }
+    // row sums over the group (cvrp/env.py:92 done; :146-148 the depot column)
+    cnt = grp_reduce<16>(cnt, [](uint32_t p, uint32_t q) { return p + q; });
+    const bool anyf = ((__ballot(feas) >> (16 * grp)) & 0xffffull) != 0ull;
+    const uint32_t dep = !((a_raw == 0) && anyf);
+    uint8_t* vdst = vis_out + byte0;
+    uint8_t* mdst = mask + byte0;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int k = sl + 16 * j;
+      const int cb = 4 * k - s;
+      if (!valid || k >= ndw) continue;
+      uint32_t mk = m[j];
+      if (cb <= 0) mk |= dep << (8 * -cb);
+      const int lo = cb < 0 ? -cb : 0;
+      const int hi = NC - cb < 4 ? NC - cb : 4;
+      if (lo == 0 && hi == 4) {
+        reinterpret_cast<uint32_t*>(vdst - s)[k] = v[j];
+        reinterpret_cast<uint32_t*>(mdst - s)[k] = mk;
+      } else {  // the row's first / last dword: its own bytes only
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (e >= lo && e < hi) {
+            vdst[cb + e] = (uint8_t)(v[j] >> (8 * e));
+            mdst[cb + e] = (uint8_t)(mk >> (8 * e));
+          }
+        }
+      }
+    }
+    if (valid) {  // the row scalars, spread over the group's lanes
+      if (sl == 0) used_out[b] = u;
+      if (sl == 1 && cur_out) cur_out[b] = a_raw;
+      if (sl == 2) done[b] = (int)cnt == NC;
+      if (sl == 3) reward[b] = 0;
+    }
+    left = valid && sl == 0 && (int)cnt != NC;
+  }
+  if (not_done) {  // one atomic per workgroup (the counter of rows not done)
+    const int wl = __popcll(__ballot(left != 0));
+    if (lane == 0) s_left[w] = wl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int q = 0; q < WAVES; ++q) t += s_left[q];
+      if (t) atomicAdd(not_done, t);
     }
   }
 }
@@ -969,6 +1113,39 @@ extern "C" int co_cvrp_step(int64_t B, int64_t N, const int64_t* action, const f
   const bool aligned = ((reinterpret_cast<uintptr_t>(vis_in) | reinterpret_cast<uintptr_t>(vis_out) |
                          reinterpret_cast<uintptr_t>(mask) | reinterpret_cast<uintptr_t>(demand)) &
                         15) == 0;
+  // wave-per-quad kernel: 4-byte-aligned byte rows, a 16-byte-aligned demand block
+  const bool quad_ok =
+      N >= 3 && N <= 252 &&
+      ((reinterpret_cast<uintptr_t>(vis_in) | reinterpret_cast<uintptr_t>(vis_out) |
+        reinterpret_cast<uintptr_t>(mask)) & 3) == 0 &&
+      (reinterpret_cast<uintptr_t>(demand) & 15) == 0;
+  if (CO_CVRP_QUAD && quad_ok) {
+    const int kpl = (int)((NC + 6) / 4 + 15) / 16;  // dwords per lane: ceil(ceil((N+4)/4) / 16)
+    const size_t slice = (size_t)(8 + 4 * N) * sizeof(float);
+    // 16 waves (64 rows) per workgroup when the not-done counter is wanted (one atomic per
+    // workgroup), else 4
+    const int waves = (not_done && 16 * slice <= 64 * 1024) ? 16 : 4;
+    const int64_t quads = (B + 3) / 4;
+    const unsigned grid = (unsigned)((quads + waves - 1) / waves);
+    hipStream_t s = (hipStream_t)stream;
+#define CO_CQ(K, W)                                                                          \
+  hipLaunchKernelGGL((cvrp_step_quad_kernel<K, W>), dim3(grid), dim3(64 * W), W * slice, s, B, \
+                     (int)N, action, demand, used_in, used_out, vcap, vis_in, vis_out, cur_out, \
+                     done, reward, mask, status, not_done)
+#define CO_CQK(W)                 \
+  if (kpl == 1) CO_CQ(1, W);      \
+  else if (kpl == 2) CO_CQ(2, W); \
+  else if (kpl == 3) CO_CQ(3, W); \
+  else CO_CQ(4, W);
+    if (waves == 16) {
+      CO_CQK(16)
+    } else {
+      CO_CQK(4)
+    }
+#undef CO_CQK
+#undef CO_CQ
+    return launch_status();
+  }
   int R = (int)((256 * kCvrpCpt * 16) / NC);
   R = (R > kCvrpMaxRows ? kCvrpMaxRows : R) & ~15;
   if (N >= 16 && aligned && R >= 16 && (size_t)R * N * sizeof(float) + 16 <= 64 * 1024) {

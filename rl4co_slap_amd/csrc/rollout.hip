@@ -369,20 +369,6 @@ __host__ __device__ inline size_t tsp_rows_wave_bytes(int gpw, int N) {
   return (((size_t)gpw * N * 8 + 15) & ~(size_t)15) * 2;
 }
 
-// The wave copies `nbytes` (16-byte aligned source and destination) global -> LDS with
-// LDS-DMA, 1 KiB per instruction; the caller waits (vmcnt) before reading.
-__device__ __forceinline__ void wave_dma(const unsigned char* __restrict__ src, int nbytes,
-                                         unsigned char* dst) {
-  const int lane = lane_id(), n16 = nbytes & ~15;
-  for (int base = 0; base < n16; base += 1024) {
-    if (base + lane * 16 < n16)
-      __builtin_amdgcn_global_load_lds((const void*)(src + base + lane * 16),
-                                       (lds_void*)(dst + base), 16, 0, 0);
-  }
-  if (lane < ((nbytes - n16) >> 2))  // an 8-byte tail (odd N): plain loads
-    reinterpret_cast<uint32_t*>(dst + n16)[lane] = reinterpret_cast<const uint32_t*>(src + n16)[lane];
-}
-
 // MODE 0: scalar 8-byte action loads; 1: 16-byte vectors (16-byte aligned rows); 2: the
 // wave's GPW action and coordinate rows (contiguous: sb == N, consecutive coordinate
 // rows) staged by LDS-DMA as two contiguous blocks, steps and gathers then read from LDS.

@@ -141,9 +141,10 @@ def test_cvrp_random_feasible_episode(dev, b, n):
     assert_reward_close(env.get_reward(td, acts.to(dev)), ref_env.get_reward(td_ref, acts))
 
 
-def _cvrp_step_raw(td, action, offset=0, not_done=None):
+def _cvrp_step_raw(td, action, offset=0, not_done=None, inplace=False):
     """co_cvrp_step on copies of the state; `offset` bytes shift the visited / mask
-    buffers off 16-B alignment (the per-instance fallback kernel)."""
+    buffers off 16-B alignment (4: the quad kernel still applies; 3: the per-instance
+    fallback kernel); `inplace` updates the visited buffer in place."""
     from rl4co_slap_amd import _native as nat
 
     b, n = td["demand"].shape
@@ -157,6 +158,8 @@ def _cvrp_step_raw(td, action, offset=0, not_done=None):
 
     vis_in = shifted(td["visited"])
     vis_out, mask = shifted(td["visited"]), shifted(td["action_mask"])
+    if inplace:
+        vis_out = vis_in
     used_out = torch.empty_like(td["used_capacity"])
     cur = torch.empty((b, 1), dtype=torch.int64, device=dev)
     done = torch.empty(b, dtype=torch.bool, device=dev)
@@ -171,10 +174,15 @@ def _cvrp_step_raw(td, action, offset=0, not_done=None):
             "current_node": cur, "done": done, "reward": rew, "status": status}
 
 
-# tile rows R = min(64, 8192 // (N+1)) & ~15: N=100 -> 64, N=200 -> 32, N=511 -> 16;
-# N=600, N < 16 and misaligned buffers take the per-instance kernel
-@pytest.mark.parametrize("b,n,offset", [(70, 100, 0), (70, 100, 3), (41, 200, 0), (19, 511, 0),
-                                        (9, 600, 0), (64, 15, 0)])
+# 3 <= N <= 252 with 4-B-aligned byte rows and a 16-B-aligned demand block: the quad kernel
+# (16 lanes per row, up to 4 dwords per lane; partial quads when B % 4 != 0); N <= 511 aligned:
+# the tile kernel (R = min(64, 8192 // (N+1)) & ~15 rows); N = 600 and misaligned buffers
+# take the per-instance kernel
+@pytest.mark.parametrize("b,n,offset", [(70, 100, 0), (70, 100, 3), (70, 100, 4), (41, 200, 0),
+                                        (19, 511, 0), (3, 256, 0), (9, 600, 0), (64, 15, 0),
+                                        (5, 3, 0), (6, 4, 0), (13, 63, 0), (11, 64, 0),
+                                        (9, 255, 0), (7, 252, 0), (1, 100, 0), (2, 37, 0),
+                                        (5, 97, 4), (3, 98, 0), (5, 99, 0)])
 def test_cvrp_step_tile_paths_and_not_done(dev, b, n, offset):
     ref_env, td_ref, env, td = _cvrp_pair(b, n, 4242 + n, dev)
     g = torch.Generator().manual_seed(5)
@@ -184,7 +192,7 @@ def test_cvrp_step_tile_paths_and_not_done(dev, b, n, offset):
         td_ref["action"] = a
         td_ref = ref_env.step(td_ref)["next"]
         nd = torch.zeros(1, dtype=torch.int32, device=dev)
-        out = _cvrp_step_raw(td, a.to(dev), offset, nd)
+        out = _cvrp_step_raw(td, a.to(dev), offset, nd, inplace=(t % 2 == 1))
         for k in ("visited", "action_mask", "used_capacity", "current_node", "done", "reward"):
             assert_same(out[k], td_ref[k], f"{k}@{t}")
         assert int(nd.item()) == int((~td_ref["done"]).sum()), t
