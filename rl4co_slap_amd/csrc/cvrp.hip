@@ -124,7 +124,13 @@ __global__ __launch_bounds__(256) void cvrp_step_kernel(
 // the mask tile is written once by a 16-B store.  `not_done` (optional) receives one
 // atomicAdd per workgroup: the number of its rows that are not done.
 #ifndef CO_CVRP_QUAD
-#define CO_CVRP_QUAD 1  // co_cvrp_step takes the wave-per-quad kernel (below) when it can
+#define CO_CVRP_QUAD 1  // co_cvrp_step takes the row-group kernel (below) when it can
+#endif
+#ifndef CO_CVRP_Q
+#define CO_CVRP_Q 1  // row groups per wave in the row-group kernel
+#endif
+#ifndef CO_CVRP_G
+#define CO_CVRP_G 16  // lanes per row in the row-group kernel
 #endif
 #ifndef CO_CVRP_ROWS
 #define CO_CVRP_ROWS 64
@@ -321,137 +327,182 @@ __global__ __launch_bounds__(THREADS) void cvrp_step_tile_kernel(
   }
 }
 
-// Quad step (cvrp/env.py:73-149, the env step the tile kernel above also implements): one
-// wave owns 4 consecutive rows (a "quad"), 16 lanes per row.  The quad's [4, N] demand rows
-// are one contiguous 16N-byte block, staged into the wave's LDS slice by LDS-DMA; the
-// visited / action_mask rows (N+1 bytes, not 4-byte aligned) are read and written in place
-// as the aligned dwords that cover the row: lane sl of a row's group owns dwords
-// k = sl + 16j of it, byte e of dword k is column 4k + e - s (s: the row's first byte
-// within its first dword).  So every row-uniform value (action, used / vehicle capacity,
-// the row sums) is group-uniform, the per-dword work is word-wide (SWAR) except the f32
-// capacity test `demand + used > capacity` per byte, and the row reductions are 16-lane
-// DPP / ballot operations.  Interior dwords are stored whole; the row's first and last
-// dword, shared with the neighbouring rows, by byte stores of the row's own bytes.  No
-// workgroup barrier on the data path; `not_done` (optional): one atomic per workgroup.
-template <int U, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) void cvrp_step_quad_kernel(
+// Row-group step (cvrp/env.py:73-149, the env step the tile kernel above also
+// implements): 16 lanes per row, 4 rows per wave, Q groups of 4 consecutive rows ("quads")
+// per wave whose loads are all issued before the first quad is computed (the compiler's
+// counted vmcnt lets quad i's work overlap quads i+1.. still in flight).  The visited /
+// action_mask rows (N+1 bytes, not 4-byte aligned) are read and written in place as the
+// aligned dwords that cover the row: lane sl owns dwords k = sl + 16j of it, byte e of
+// dword k is column 4k + e - s (s: the row's first byte within its first dword).  The
+// demand of those 4 columns is one 4-byte-aligned float4 load (demand[4k - s - 1 ...]).
+// Row-uniform values (action, used / vehicle capacity) are group-uniform; the selected
+// demand (the action's column) comes from the lane that holds it by a 16-lane OR
+// reduction, so no load depends on another.  Per dword only the f32 capacity test
+// `demand + used > capacity` runs per byte; the action byte, the nonzero test, the byte
+// sums (v_sad_u8) and the customer mask are word-wide; the row sums (done, the depot
+// column) are 16-lane DPP / ballot operations.  Interior dwords are stored whole, the
+// row's first and last dword (shared with the neighbouring rows) as its own bytes.  No
+// LDS, no workgroup barrier on the data path; `not_done` (optional): one atomic per
+// workgroup.
+typedef float f4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+template <int G, int U, int Q, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void cvrp_step_rows_kernel(
     int64_t B, int N, const int64_t* __restrict__ action, const float* __restrict__ demand,
     const float* __restrict__ used_in, float* __restrict__ used_out,
     const float* __restrict__ vcap, const uint8_t* vis_in, uint8_t* vis_out,
     int64_t* __restrict__ cur_out, uint8_t* __restrict__ done, uint8_t* __restrict__ reward,
     uint8_t* __restrict__ mask, int32_t* status, int32_t* not_done) {
-  extern __shared__ __attribute__((aligned(16))) float s_quad[];  // per wave: 4 + 4N + 4 floats
   __shared__ int s_left[WAVES];
-  const int lane = lane_id(), w = threadIdx.x >> 6, sl = lane & 15, grp = lane >> 4;
+  constexpr int RW = 64 / G;  // rows per wave
+  const int lane = lane_id(), w = threadIdx.x >> 6, sl = lane % G, grp = lane / G;
   const int NC = N + 1;
-  float* const sd = s_quad + w * (8 + 4 * N) + 4;
-  const int64_t row0 = ((int64_t)blockIdx.x * WAVES + w) * 4;
+  const int64_t wrow0 = ((int64_t)blockIdx.x * WAVES + w) * (RW * Q);
   int left = 0;
-  if (row0 < B) {
-    const int rows = (int)(B - row0 < 4 ? B - row0 : 4);
-    const bool valid = grp < rows;
-    const int64_t b = valid ? row0 + grp : row0;
-    // every global load before the one wait: the row scalars (group-uniform addresses)
-    const int64_t a_raw = action[b];
-    const float uin = used_in[b], cap = vcap[b];
-    const int64_t byte0 = b * NC;
-    const int s = (int)(byte0 & 3);
-    const int ndw = (s + NC + 3) >> 2;  // dwords covering the row
-    const uint32_t* vrow = reinterpret_cast<const uint32_t*>(vis_in) + (byte0 >> 2);
-    uint32_t v[U];
+  if (wrow0 < B) {
+    // ---- every load of the wave's Q quads (rows past B re-read row B-1: not stored)
+    int64_t A[Q];
+    float UI[Q], CP[Q];
+    uint32_t V[Q][U];
+    f4_a4 D[Q][U];
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const int k = sl + 16 * j;
-      v[j] = 0u;
-      if (valid && k < ndw) {
+    for (int q = 0; q < Q; ++q) {
+      const int64_t b0 = wrow0 + RW * q + grp;
+      const int64_t b = b0 < B ? b0 : B - 1;
+      A[q] = action[b];
+      UI[q] = used_in[b];
+      CP[q] = vcap[b];
+      const int64_t byte0 = b * NC;
+      const int s = (int)(byte0 & 3);
+      const int ndw = (s + NC + 3) >> 2;
+      const uint32_t* vrow = reinterpret_cast<const uint32_t*>(vis_in + (byte0 - s));
+      const float* drow = demand + b * N;
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int k0 = sl + G * j;
+        const int k = k0 < ndw ? k0 : 0;
+        const int cb = 4 * k - s;
         if (b == B - 1 && k == ndw - 1 && ((byte0 + NC) & 3)) {  // the buffer's last bytes
+          uint32_t x = 0u;
 #pragma unroll
           for (int e = 0; e < 3; ++e)
-            if (e < ((byte0 + NC) & 3)) v[j] |= (uint32_t)vis_in[byte0 - s + 4 * k + e] << (8 * e);
+            if (e < ((byte0 + NC) & 3)) x |= (uint32_t)vis_in[byte0 - s + 4 * k + e] << (8 * e);
+          V[q][j] = x;
         } else {
-          v[j] = vrow[k];
+          V[q][j] = vrow[k];
+        }
+        if ((b == 0 && cb < 1) || (b == B - 1 && cb + 2 > N - 1)) {
+          // the buffer's first / last row: out-of-row elements clamped (they belong to no
+          // customer byte of this row)
+          f4_a4 d;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int ix = cb - 1 + e;
+            d[e] = drow[ix < 0 ? 0 : (ix > N - 1 ? N - 1 : ix)];
+          }
+          D[q][j] = d;
+        } else {
+          D[q][j] = *reinterpret_cast<const f4_a4*>(drow + (cb - 1));
         }
       }
     }
-    wave_dma(reinterpret_cast<const unsigned char*>(demand + row0 * N), rows * N * 4,
-             reinterpret_cast<unsigned char*>(sd));
-    wave_dma_wait();
-    // cvrp/env.py:79-85
-    const bool bad = a_raw < 0 || a_raw > N;
-    if (valid && bad && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
-    const float* drow = sd + grp * N;
-    int64_t di = a_raw - 1;
-    di = di < 0 ? 0 : (di > N - 1 ? N - 1 : di);
-    const float u = (uin + drow[di]) * ((a_raw != 0) ? 1.0f : 0.0f);
-    const int a = bad ? -1 : (int)a_raw;
-    uint32_t m[U];
-    uint32_t cnt = 0u;
-    bool feas = false;
+    // ---- per quad: cvrp/env.py:79-92 and get_action_mask (:137-149)
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const int k = sl + 16 * j;
-      const bool live = valid && k < ndw;
-      const int cb = live ? 4 * k - s : 0;  // column of byte 0 (dead slots: dword 0's)
-      // the row's own bytes [lo, hi) of this dword; the depot byte (column 0) at -cb
-      const int lo = cb < 0 ? -cb : 0;
-      const int hi = NC - cb < 4 ? NC - cb : 4;
-      const uint32_t own = !live ? 0u
-                           : ((hi >= 4 ? 0xffffffffu : (1u << (8 * hi)) - 1u) &
-                              ~((1u << (8 * lo)) - 1u));
-      const uint32_t cust = cb <= 0 ? own & ~(0xffu << (8 * lo)) : own;  // depot excluded
-      uint32_t x = v[j];
-      const int ea = a - cb;  // the action's byte, if in this dword
-      if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
-      v[j] = x;
-      // demand of byte e: drow[cb + e - 1] (the slice's pad covers cb - 1 >= -4 and N + 2)
-      const float* dp = drow + (cb - 1);
-      uint32_t over = 0u;
+    for (int q = 0; q < Q; ++q) {
+      const int64_t b = wrow0 + RW * q + grp;
+      const bool valid = b < B;
+      const int64_t bb = valid ? b : B - 1;
+      const int64_t a_raw = A[q];
+      const bool bad = a_raw < 0 || a_raw > N;
+      if (valid && bad && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
+      const int64_t byte0 = bb * NC;
+      const int s = (int)(byte0 & 3);
+      const int ndw = (s + NC + 3) >> 2;
+      // the selected demand demand[clamp(a - 1, 0, N - 1)] from the lane holding it
+      const int csel = (int)(a_raw - 1 < 0 ? 0 : (a_raw - 1 > N - 1 ? N - 1 : a_raw - 1)) + 1;
+      uint32_t selb = 0u;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) over |= (dp[e] + u > cap) ? (0x80u << (8 * e)) : 0u;
-      const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
-      const uint32_t mk = ((~(nz | over) & 0x80808080u) >> 7) & cust;
-      cnt = __builtin_amdgcn_sad_u8(x & own, 0u, cnt);
-      feas |= mk != 0u;
-      m[j] = mk;
-    }
-    // row sums over the group (cvrp/env.py:92 done; :146-148 the depot column)
-    cnt = grp_reduce<16>(cnt, [](uint32_t p, uint32_t q) { return p + q; });
-    const bool anyf = ((__ballot(feas) >> (16 * grp)) & 0xffffull) != 0ull;
-    const uint32_t dep = !((a_raw == 0) && anyf);
-    uint8_t* vdst = vis_out + byte0;
-    uint8_t* mdst = mask + byte0;
+      for (int j = 0; j < U; ++j) {
+        const int k = sl + G * j;
+        const int es = csel - (4 * k - s);
+        if (k < ndw && es >= 0 && es < 4) {
+          const f4_a4 d = D[q][j];
+          selb = __float_as_uint(es == 0 ? d[0] : es == 1 ? d[1] : es == 2 ? d[2] : d[3]);
+        }
+      }
+      selb = grp_reduce<G>(selb, [](uint32_t x, uint32_t y) { return x | y; });
+      const float u = (UI[q] + __uint_as_float(selb)) * ((a_raw != 0) ? 1.0f : 0.0f);
+      const float cap = CP[q];
+      const int a = bad ? -1 : (int)a_raw;
+      uint32_t m[U];
+      uint32_t cnt = 0u;
+      bool feas = false;
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const int k = sl + 16 * j;
-      const int cb = 4 * k - s;
-      if (!valid || k >= ndw) continue;
-      uint32_t mk = m[j];
-      if (cb <= 0) mk |= dep << (8 * -cb);
-      const int lo = cb < 0 ? -cb : 0;
-      const int hi = NC - cb < 4 ? NC - cb : 4;
-      if (lo == 0 && hi == 4) {
-        reinterpret_cast<uint32_t*>(vdst - s)[k] = v[j];
-        reinterpret_cast<uint32_t*>(mdst - s)[k] = mk;
-      } else {  // the row's first / last dword: its own bytes only
+      for (int j = 0; j < U; ++j) {
+        const int k = sl + G * j;
+        const bool live = valid && k < ndw;
+        const int cb = live ? 4 * k - s : 0;  // column of byte 0 (dead slots: dword 0's)
+        // the row's own bytes [lo, hi) of this dword; the depot byte (column 0) at -cb
+        const int lo = cb < 0 ? -cb : 0;
+        const int hi = NC - cb < 4 ? NC - cb : 4;
+        const uint32_t own = !live ? 0u
+                             : ((hi >= 4 ? 0xffffffffu : (1u << (8 * hi)) - 1u) &
+                                ~((1u << (8 * lo)) - 1u));
+        const uint32_t cust = cb <= 0 ? own & ~(0xffu << (8 * lo)) : own;  // depot excluded
+        uint32_t x = V[q][j];
+        const int ea = a - cb;  // the action's byte, if in this dword
+        if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
+        V[q][j] = x;
+        const f4_a4 d = D[q][j];
+        const uint32_t over = ((d[0] + u > cap) ? 0x80u : 0u) | ((d[1] + u > cap) ? 0x8000u : 0u) |
+                              ((d[2] + u > cap) ? 0x800000u : 0u) |
+                              ((d[3] + u > cap) ? 0x80000000u : 0u);
+        const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+        const uint32_t mk = ((~(nz | over) & 0x80808080u) >> 7) & cust;
+        cnt = __builtin_amdgcn_sad_u8(x & own, 0u, cnt);
+        feas |= mk != 0u;
+        m[j] = mk;
+      }
+      // row sums over the group (cvrp/env.py:92 done; :146-148 the depot column)
+      cnt = grp_reduce<G>(cnt, [](uint32_t x, uint32_t y) { return x + y; });
+      const uint64_t gm = G == 64 ? ~0ull : ((1ull << G) - 1ull);
+      const bool anyf = ((__ballot(feas) >> (G * grp)) & gm) != 0ull;
+      const uint32_t dep = !((a_raw == 0) && anyf);
+      uint8_t* vdst = vis_out + byte0;
+      uint8_t* mdst = mask + byte0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (e >= lo && e < hi) {
-            vdst[cb + e] = (uint8_t)(v[j] >> (8 * e));
-            mdst[cb + e] = (uint8_t)(mk >> (8 * e));
+      for (int j = 0; j < U; ++j) {
+        const int k = sl + G * j;
+        if (!valid || k >= ndw) continue;
+        const int cb = 4 * k - s;
+        uint32_t mk = m[j];
+        if (cb <= 0) mk |= dep << (8 * -cb);
+        const int lo = cb < 0 ? -cb : 0;
+        const int hi = NC - cb < 4 ? NC - cb : 4;
+        if (lo == 0 && hi == 4) {
+          reinterpret_cast<uint32_t*>(vdst - s)[k] = V[q][j];
+          reinterpret_cast<uint32_t*>(mdst - s)[k] = mk;
+        } else {  // the row's first / last dword: its own bytes only
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (e >= lo && e < hi) {
+              vdst[cb + e] = (uint8_t)(V[q][j] >> (8 * e));
+              mdst[cb + e] = (uint8_t)(mk >> (8 * e));
+            }
           }
         }
       }
+      if (valid) {  // the row scalars, spread over the group's lanes
+        if (sl == 0) used_out[b] = u;
+        if (sl == 1 && cur_out) cur_out[b] = a_raw;
+        if (sl == 2) done[b] = (int)cnt == NC;
+        if (sl == 3) reward[b] = 0;
+      }
+      left += valid && sl == 0 && (int)cnt != NC;
     }
-    if (valid) {  // the row scalars, spread over the group's lanes
-      if (sl == 0) used_out[b] = u;
-      if (sl == 1 && cur_out) cur_out[b] = a_raw;
-      if (sl == 2) done[b] = (int)cnt == NC;
-      if (sl == 3) reward[b] = 0;
-    }
-    left = valid && sl == 0 && (int)cnt != NC;
   }
   if (not_done) {  // one atomic per workgroup (the counter of rows not done)
-    const int wl = __popcll(__ballot(left != 0));
+    const int wl = (int)wave_sum((uint32_t)left);
     if (lane == 0) s_left[w] = wl;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1113,23 +1164,23 @@ extern "C" int co_cvrp_step(int64_t B, int64_t N, const int64_t* action, const f
   const bool aligned = ((reinterpret_cast<uintptr_t>(vis_in) | reinterpret_cast<uintptr_t>(vis_out) |
                          reinterpret_cast<uintptr_t>(mask) | reinterpret_cast<uintptr_t>(demand)) &
                         15) == 0;
-  // wave-per-quad kernel: 4-byte-aligned byte rows, a 16-byte-aligned demand block
-  const bool quad_ok =
+  // row-group kernel: 4-byte-aligned byte rows and demand
+  const bool rows_ok =
       N >= 3 && N <= 252 &&
       ((reinterpret_cast<uintptr_t>(vis_in) | reinterpret_cast<uintptr_t>(vis_out) |
-        reinterpret_cast<uintptr_t>(mask)) & 3) == 0 &&
-      (reinterpret_cast<uintptr_t>(demand) & 15) == 0;
-  if (CO_CVRP_QUAD && quad_ok) {
-    const int kpl = (int)((NC + 6) / 4 + 15) / 16;  // dwords per lane: ceil(ceil((N+4)/4) / 16)
-    const size_t slice = (size_t)(8 + 4 * N) * sizeof(float);
-    // 16 waves (64 rows) per workgroup when the not-done counter is wanted (one atomic per
-    // workgroup), else 4
-    const int waves = (not_done && 16 * slice <= 64 * 1024) ? 16 : 4;
-    const int64_t quads = (B + 3) / 4;
-    const unsigned grid = (unsigned)((quads + waves - 1) / waves);
+        reinterpret_cast<uintptr_t>(mask) | reinterpret_cast<uintptr_t>(demand)) & 3) == 0;
+  constexpr int G = CO_CVRP_G, Q = CO_CVRP_Q;
+  // dwords per lane: ceil(ceil((N+4)/4) / G), at most 4
+  const int kpl = (int)((NC + 6) / 4 + G - 1) / G;
+  if (CO_CVRP_QUAD && rows_ok && kpl <= 4) {
+    // 16 waves per workgroup when the not-done counter is wanted (fewer atomics), else 4
+    const int waves = not_done ? 16 : 4;
+    const int64_t rows_per_wg = (int64_t)(64 / G) * Q * waves;
+    const int64_t wgs = (B + rows_per_wg - 1) / rows_per_wg;
+    const unsigned grid = (unsigned)wgs;
     hipStream_t s = (hipStream_t)stream;
-#define CO_CQ(K, W)                                                                          \
-  hipLaunchKernelGGL((cvrp_step_quad_kernel<K, W>), dim3(grid), dim3(64 * W), W * slice, s, B, \
+#define CO_CQ(K, W)                                                                         \
+  hipLaunchKernelGGL((cvrp_step_rows_kernel<G, K, Q, W>), dim3(grid), dim3(64 * W), 0, s, B,  \
                      (int)N, action, demand, used_in, used_out, vcap, vis_in, vis_out, cur_out, \
                      done, reward, mask, status, not_done)
 #define CO_CQK(W)                 \
