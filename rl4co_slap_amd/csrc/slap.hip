@@ -15,6 +15,10 @@
 
 using namespace co;
 
+#ifndef CO_SLAP_GROUP_STEP
+#define CO_SLAP_GROUP_STEP 1  // co_slap_step on the 16-lane group kernel when it can
+#endif
+
 namespace {
 
 __global__ __launch_bounds__(256) void slap_reset_kernel(int64_t B, int64_t L, int64_t P,
@@ -385,10 +389,14 @@ __global__ __launch_bounds__(256) void slap_closest_kernel(int64_t B, int L, con
 // group min then an index group min (grp_argmin_split); the owner lane's unit is
 // written back with the chosen byte cleared, every other unit unchanged; lane 0
 // applies the step's row epilogue (slap/env.py:38-93).
-template <int KU>
+// CLOSEST = false: the env step alone (co_slap_step) on the same group layout, the action
+// given (action_in; negative values index from the end as python indexing, out-of-range
+// ones set CO_ST_INDEX_RANGE and clear nothing, as the tile kernel).
+template <int KU, bool CLOSEST>
 __global__ __launch_bounds__(256) void slap_closest_step_kernel(
     int64_t B, int L, int P, const float* __restrict__ dist, const uint8_t* __restrict__ mask_in,
-    uint8_t* __restrict__ mask_out, int64_t* __restrict__ action_out,
+    uint8_t* __restrict__ mask_out, const int64_t* __restrict__ action_in,
+    int64_t* __restrict__ action_out,
     const float* __restrict__ to_choose, int64_t tc_stride, const int32_t* assign_in,
     int32_t* assign, const int64_t* __restrict__ i_in, int64_t* __restrict__ i_out, uint8_t* __restrict__ done,
     uint8_t* __restrict__ reward, int32_t* status) {
@@ -406,37 +414,50 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
   for (int k = 0; k < KU; ++k) {  // all loads first, unconditional within the row
     const int u = sl + G * k;
     const int uc = u < U ? u : U - 1;
-    dv[k] = drow[uc];
+    if constexpr (CLOSEST) dv[k] = drow[uc];
     mv[k] = mrow[uc];
   }
   int64_t it = 0;
   if (sl == 0) it = i_in[bb];
   const float prod = to_choose[bb * tc_stride];  // every lane (one broadcast line)
-  float best = __builtin_inff();
   int bi = 0x7fffffff;
+  int64_t a_raw = 0;
+  if constexpr (CLOSEST) {
+    float best = __builtin_inff();
 #pragma unroll
-  for (int k = 0; k < KU; ++k) {
-    const int u = sl + G * k;
-    if (u < U) {
-      const float d4[4] = {dv[k].x, dv[k].y, dv[k].z, dv[k].w};
+    for (int k = 0; k < KU; ++k) {
+      const int u = sl + G * k;
+      if (u < U) {
+        const float d4[4] = {dv[k].x, dv[k].y, dv[k].z, dv[k].w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = ((mv[k] >> (8 * j)) & 0xffu) ? d4[j] : __builtin_inff();
-        if (d < best) {  // ascending index within the lane: strict < keeps the lowest
-          best = d;
-          bi = 4 * u + j;
+        for (int j = 0; j < 4; ++j) {
+          const float d = ((mv[k] >> (8 * j)) & 0xffu) ? d4[j] : __builtin_inff();
+          if (d < best) {  // ascending index within the lane: strict < keeps the lowest
+            best = d;
+            bi = 4 * u + j;
+          }
         }
+        if (bi == 0x7fffffff) bi = 4 * u;  // a lane whose candidates are all masked
       }
-      if (bi == 0x7fffffff) bi = 4 * u;  // a lane whose candidates are all masked
     }
+    grp_argmin_split<G>(best, bi);
+    a_raw = bi;
+  } else {
+    a_raw = action_in[bb];  // group-uniform address (one request)
+    int64_t a = a_raw < 0 ? a_raw + L : a_raw;  // slap/env.py:46 (python indexing)
+    if (a < 0 || a >= L) {
+      if (live && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
+      a = -1;
+    }
+    bi = (int)a;  // -1: no byte cleared
   }
-  grp_argmin_split<G>(best, bi);
   if (!live) return;
   int64_t p = (int64_t)(int)prod;  // .to(torch.int), slap/env.py:52
   if (p < 0) p += P;
   const bool p_ok = p >= 0 && p < P;
+  const int32_t av = (int32_t)a_raw;  // .to(torch.int), slap/env.py:53-54
   if (assign_in != assign)  // out of place: the group writes the row with [p] = action
-    for (int c = sl; c < P; c += G) assign[b * P + c] = c == p ? bi : assign_in[b * P + c];
+    for (int c = sl; c < P; c += G) assign[b * P + c] = c == p ? av : assign_in[b * P + c];
   uint32_t* mo = reinterpret_cast<uint32_t*>(mask_out + b * (int64_t)L);
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
@@ -447,11 +468,11 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
     }
   }
   if (sl == 0) {  // slap/env.py:50-62 (the row epilogue of co_slap_step)
-    action_out[b] = bi;
+    if constexpr (CLOSEST) action_out[b] = bi;
     if (!p_ok)
       set_status(status, CO_ST_INDEX_RANGE);
     else if (assign_in == assign)
-      assign[b * P + p] = bi;
+      assign[b * P + p] = av;
     done[b] = it == (int64_t)(P - 1);
     i_out[b] = it + 1;
     reward[b] = 0;
@@ -480,6 +501,26 @@ extern "C" int co_slap_step(int64_t B, int64_t L, int64_t P, const int64_t* acti
   if (!action || !to_choose || !assign_in || !assign_out || !mask_in || !mask_out || !i_in ||
       !i_out || !done || !reward)
     return CO_E_INVAL;
+  // 16 lanes per instance (the closest-step layout without the policy) for L % 4 == 0,
+  // L <= 256 and 4-B-aligned mask rows; else the 64-row byte tile
+  if (CO_SLAP_GROUP_STEP && L % 4 == 0 && L <= 256 &&
+      ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) & 3) == 0) {
+    const dim3 grid((unsigned)((B + 15) / 16));
+    const int ku = (int)((L / 4 + 15) / 16);
+#define CO_SLAP_GS(K)                                                                         \
+  hipLaunchKernelGGL((slap_closest_step_kernel<K, false>), grid, dim3(256), 0,               \
+                     (hipStream_t)stream, B, (int)L, (int)P, nullptr, mask_in, mask_out, action, \
+                     nullptr, to_choose, tc_stride, assign_in, assign_out, i_in, i_out, done,  \
+                     reward, status)
+    switch (ku) {
+      case 1: CO_SLAP_GS(1); break;
+      case 2: CO_SLAP_GS(2); break;
+      case 3: CO_SLAP_GS(3); break;
+      default: CO_SLAP_GS(4);
+    }
+#undef CO_SLAP_GS
+    return launch_status();
+  }
   SlapRowEpilogue epi{(int)P, to_choose, tc_stride, assign_out, i_in, i_out, done, reward,
                       status};
   const unsigned grid = (unsigned)((B + kTileRows - 1) / kTileRows);
@@ -572,8 +613,8 @@ extern "C" int co_slap_closest_step(int64_t B, int64_t L, int64_t P, const float
   const dim3 grid((unsigned)((B + 15) / 16));
   const int units = (int)(L / 4), ku = (units + 15) / 16;
 #define CO_SLAP_CS(K)                                                                        \
-  hipLaunchKernelGGL(slap_closest_step_kernel<K>, grid, dim3(256), 0, (hipStream_t)stream, B, \
-                     (int)L, (int)P, dist, mask_in, mask_out, action_out, to_choose, tc_stride, \
+  hipLaunchKernelGGL((slap_closest_step_kernel<K, true>), grid, dim3(256), 0, (hipStream_t)stream, \
+                     B, (int)L, (int)P, dist, mask_in, mask_out, nullptr, action_out, to_choose, tc_stride, \
                      assign_in, assign, i_in, i_out, done, reward, status)
   switch (ku) {
     case 1: CO_SLAP_CS(1); break;

@@ -82,9 +82,6 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
 #ifndef CO_TSP_LAYOUT
 #define CO_TSP_LAYOUT 1
 #endif
-#ifndef CO_TSP_XCD
-#define CO_TSP_XCD 0
-#endif
 #ifndef CO_TSP_SCUT
 #define CO_TSP_SCUT 0  // timing diagnostic only: 1 no row epilogue, 2 no mask store
 #endif
@@ -101,13 +98,7 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
   const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
   const int W = N >> 2;  // words per row
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  // CO_TSP_XCD: consecutive workgroups go round-robin to the 8 XCDs (separate L2s); map
-  // them so each XCD owns one contiguous range of rows, and a cache line of the 1-byte
-  // done / reward columns is written from one L2
-  const unsigned bid = (CO_TSP_XCD && (gridDim.x & 7) == 0)
-                           ? (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3)
-                           : blockIdx.x;
-  const int64_t wid = (int64_t)bid * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
   if (first_mode == 2) epi.take_first = (*first_flag != 0);
   for (int64_t base = wid * (64 / G); base < B; base += nwaves * (64 / G)) {

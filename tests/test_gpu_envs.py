@@ -285,6 +285,69 @@ def test_slap_episode(dev, b):
     assert_reward_close(env.get_reward(td, None), ref_env.get_reward(td_ref, None))
 
 
+def _slap_step_raw(td, action, inplace, offset=0):
+    """co_slap_step on copies of the state (`offset` bytes shift the mask buffers off 4-B
+    alignment: the byte-tile kernel instead of the 16-lane group kernel)."""
+    from rl4co_slap_amd import _native as nat
+
+    b, l = td["action_mask"].shape
+    p = td["assignment"].shape[1]
+    dev = action.device
+
+    def shifted(x):
+        flat = torch.empty(x.numel() + 16, dtype=torch.uint8, device=dev)
+        v = flat[offset:offset + x.numel()].view(x.shape)
+        v.copy_(x.view(torch.uint8))
+        return v
+
+    m_in, m_out = shifted(td["action_mask"]), shifted(td["action_mask"])
+    a_in = td["assignment"].clone()
+    a_out = a_in if inplace else torch.full_like(a_in, 12345)
+    i_out = torch.empty_like(td["i"])
+    done = torch.empty((b, 1), dtype=torch.bool, device=dev)
+    rew = torch.empty((b, 1), dtype=torch.bool, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    tc = td["to_choose"]
+    nat.call("co_slap_step", b, l, p, nat.ptr(action), nat.ptr(tc), tc.stride(0), nat.ptr(a_in),
+             nat.ptr(a_out), nat.ptr(m_in), nat.ptr(m_out), nat.ptr(td["i"]), nat.ptr(i_out),
+             nat.ptr(done), nat.ptr(rew), nat.ptr(st), nat.stream_of(action))
+    return {"action_mask": m_out.view(torch.bool), "assignment": a_out, "i": i_out, "done": done,
+            "reward": rew, "status": st}
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_slap_step_group_and_tile_paths(dev, offset):
+    # negative actions index from the end (python indexing); in- and out-of-place
+    # assignment; an out-of-range action flags CO_ST_INDEX_RANGE and clears nothing
+    import rl4co_slap_amd as ra
+
+    b = 37
+    ref_env = SLAPOracle(seed=5)
+    np.random.seed(5)
+    gen = ref_env.generate([b])
+    td_ref = ref_env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    env = SLAPEnv(seed=1, device=dev)
+    td = env.reset(ra.TensorDict({k: v.clone() for k, v in gen.items()}, [b]))
+    bad = torch.ones(b, dtype=torch.int64, device=dev)
+    bad[4] = 100
+    out = _slap_step_raw(td, bad, inplace=False, offset=offset)
+    assert int(out["status"].item()) & 8
+    assert torch.equal(out["action_mask"][4].cpu(), td["action_mask"][4].cpu())
+    assert not torch.equal(out["action_mask"][3].cpu(), td["action_mask"][3].cpu())
+    g = torch.Generator().manual_seed(9)
+    for t in range(20):
+        a = torch.multinomial(td_ref["action_mask"].float(), 1, generator=g).squeeze(-1)
+        a[t % 3::3] -= 100  # the same locations, written python-negative
+        out = _slap_step_raw(td, a.to(dev), inplace=(t % 2 == 1), offset=offset)
+        td_ref["action"] = a
+        td_ref = ref_env.step(td_ref)["next"]
+        for k in ("action_mask", "assignment", "i", "done", "reward"):
+            assert_same(out[k], td_ref[k], f"{k}@{t}")
+        assert int(out["status"].item()) == 0
+        td["action"] = a.to(dev)
+        td = env.step(td)["next"]
+
+
 def test_slap_reward_partial_assignment_wraps(dev):
     # unassigned products (-1) index the last location, like python indexing
     import rl4co_slap_amd as ra
