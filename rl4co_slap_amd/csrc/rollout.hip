@@ -702,7 +702,8 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
   if (CLOSEST) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
-      const uint32_t u = __float_as_uint(dd[k]);
+      // -0.0 keyed as +0.0: they tie (argmin's float compare), the index decides
+      const uint32_t u = dd[k] == 0.f ? 0u : __float_as_uint(dd[k]);
       const uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
       key[k] = ((uint64_t)ord << 32) | (uint32_t)(sl + G * k);
     }

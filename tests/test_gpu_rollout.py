@@ -198,14 +198,18 @@ def test_slap_rollout_matches_oracle(dev, cls_name, b, policy):
 @pytest.mark.parametrize("aisles,locs,prods,orders", [(6, 8, 12, 9), (12, 15, 40, 25),
                                                       (10, 10, 20, 20), (4, 5, 19, 7),
                                                       (7, 7, 20, 9)])
-@pytest.mark.parametrize("dist", ["grid", "random_ties"])
-@pytest.mark.parametrize("cls_name", ["SLAPFusedEpisode", "SLAPStepwiseEpisode"])
+@pytest.mark.parametrize("dist", ["grid", "random_ties", "zeros_inf"])
+@pytest.mark.parametrize("cls_name", ["SLAPFusedEpisode", "SLAPStepwiseEpisode",
+                                      "SLAPStepwiseEpisode:dist"])
 def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist, cls_name):
     """Closest-free episodes for every lane-group width of the fused kernel (L = 48 -> 8
     lanes, 100 -> 16, 180 -> 32), P close to L - 1 (a lane's sorted list runs dry), and
     depot distances with many exact ties at random positions; the stepwise engine's
     co_slap_closest_step (policy + step in one launch: 1 / 2 / 3 units of 4 locations
-    per lane; L = 49 takes its two-launch fallback)."""
+    per lane; L = 49 takes its two-launch fallback) -- by default from the per-episode ranks
+    of co_slap_closest_rank (co_slap_closest_step_ranked), ":dist" from the distances.
+    "zeros_inf": ties of -0.0 / +0.0 and a few +inf distances (never picked while a finite
+    free slot is left)."""
     import numpy as np
 
     import rl4co_slap_amd.rollout.engine as eng
@@ -217,14 +221,23 @@ def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist, cls_na
     env = SLAPOracle(n_products=prods, n_aisles=aisles, n_locs=locs, max_orders=orders, seed=3)
     np.random.seed(3)
     gen = env.generate([b])
-    if dist == "random_ties":
+    if dist in ("random_ties", "zeros_inf"):
         g = torch.Generator().manual_seed(9)
         gen["depot_loc_dist"] = torch.randint(0, 6, gen["depot_loc_dist"].shape,
                                               generator=g).float() * 0.5
+    if dist == "zeros_inf":
+        dd = gen["depot_loc_dist"]
+        sel = torch.rand(dd.shape, generator=g)
+        dd[(dd == 0) & (sel < 0.5)] = -0.0
+        dd[sel > 0.97] = float("inf")
     td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
     r, tdf, a = ref_rollout(env, td, slap_closest_free_action)
-    ep = getattr(eng, cls_name)(TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev),
-                                None, policy="closest")
+    kw = {"ranked": False} if cls_name.endswith(":dist") else {}
+    ep = getattr(eng, cls_name.split(":")[0])(
+        TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev), None, policy="closest",
+        **kw)
+    if cls_name == "SLAPStepwiseEpisode":
+        assert ep.ranked == (aisles * locs % 4 == 0)
     ep.run_eager()
     torch.cuda.synchronize()
     assert int(ep.status.item()) == 0
