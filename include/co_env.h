@@ -258,25 +258,6 @@ int co_slap_closest_step(int64_t batch, int64_t num_slots, int64_t n_products,
                          int64_t* action_out, const int64_t* i_in, int64_t* i_out, uint8_t* done,
                          uint8_t* reward, int32_t* status, void* stream);
 
-/* The closest-free bench policy's per-episode precomputation (not reference code; the
- * policy examples/slap.py's stepwise loop stands in for): rank_out[b, j] (u8) = the
- * position of slot j in instance b's order by (depot_loc_dist, index), 255 where the
- * distance is not finite.  num_slots % 4 == 0 and <= 252; depot_loc_dist 16-byte and
- * rank_out 4-byte aligned (CO_E_ALIGN otherwise). */
-int co_slap_closest_rank(int64_t batch, int64_t num_slots, const float* depot_loc_dist,
-                         uint8_t* rank_out, void* stream);
-
-/* co_slap_closest_step with the policy read from co_slap_closest_rank's ranks (num_slots
- * bytes per instance instead of 4 * num_slots of distances): the same actions and state,
- * bit for bit (the free slot of least rank; slot 0 when no free slot has a finite
- * distance, as the distance path).  Same shape / alignment limits as
- * co_slap_closest_rank (mask rows 4-byte aligned). */
-int co_slap_closest_step_ranked(int64_t batch, int64_t num_slots, int64_t n_products,
-                                const uint8_t* rank, const float* to_choose, int64_t tc_stride,
-                                const int32_t* assign_in, int32_t* assign_out,
-                                const uint8_t* mask_in, uint8_t* mask_out, int64_t* action_out,
-                                const int64_t* i_in, int64_t* i_out, uint8_t* done,
-                                uint8_t* reward, int32_t* status, void* stream);
 
 /* -------------------------------------------- fused episode rollouts */
 

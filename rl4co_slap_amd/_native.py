@@ -50,9 +50,6 @@ _SIGS = {
     "co_slap_closest_free_action": [_i64, _i64, _p, _p, _p, _p],
     "co_slap_closest_step": [_i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                              _p, _p],
-    "co_slap_closest_rank": [_i64, _i64, _p, _p, _p],
-    "co_slap_closest_step_ranked": [_i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p,
-                                    _p, _p, _p, _p],
     "co_count_not_done": [_p, _i64, _p, _p],
     "co_probe_copy": [_p, _p, _i64, _p],
     "co_uniform_fill": [_p, _i64, _f32, _f32, _f32, _i32, _u64, _u64, _p],

@@ -392,11 +392,7 @@ __global__ __launch_bounds__(256) void slap_closest_kernel(int64_t B, int L, con
 // CLOSEST = false: the env step alone (co_slap_step) on the same group layout, the action
 // given (action_in; negative values index from the end as python indexing, out-of-range
 // ones set CO_ST_INDEX_RANGE and clear nothing, as the tile kernel).
-// RANKED (with CLOSEST): `dist` is the u8 rank row of co_slap_closest_rank (the order by
-// (distance, index); 255: not finite) -- one u32 per unit instead of a float4, the pick
-// is the free location of least rank (a 16-bit (rank, index) group min), location 0 when
-// no free location has a finite distance (as the distance path's all-inf argmin).
-template <int KU, bool CLOSEST, bool RANKED = false>
+template <int KU, bool CLOSEST>
 __global__ __launch_bounds__(256) void slap_closest_step_kernel(
     int64_t B, int L, int P, const float* __restrict__ dist, const uint8_t* __restrict__ mask_in,
     uint8_t* __restrict__ mask_out, const int64_t* __restrict__ action_in,
@@ -412,16 +408,13 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
   const int U = L >> 2;                  // units per row (L % 4 == 0)
   const float4* drow = reinterpret_cast<const float4*>(dist + bb * (int64_t)L);
   const uint32_t* mrow = reinterpret_cast<const uint32_t*>(mask_in + bb * (int64_t)L);
-  const uint32_t* rrow = reinterpret_cast<const uint32_t*>(
-      reinterpret_cast<const uint8_t*>(dist) + bb * (int64_t)L);
   float4 dv[KU];
-  uint32_t mv[KU], rv[KU];
+  uint32_t mv[KU];
 #pragma unroll
   for (int k = 0; k < KU; ++k) {  // all loads first, unconditional within the row
     const int u = sl + G * k;
     const int uc = u < U ? u : U - 1;
-    if constexpr (CLOSEST && RANKED) rv[k] = rrow[uc];
-    else if constexpr (CLOSEST) dv[k] = drow[uc];
+    if constexpr (CLOSEST) dv[k] = drow[uc];
     mv[k] = mrow[uc];
   }
   int64_t it = 0;
@@ -429,25 +422,7 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
   const float prod = to_choose[bb * tc_stride];  // every lane (one broadcast line)
   int bi = 0x7fffffff;
   int64_t a_raw = 0;
-  if constexpr (CLOSEST && RANKED) {
-    uint32_t key = 0xffffu;  // (rank << 8) | location of the lane's free locations
-#pragma unroll
-    for (int k = 0; k < KU; ++k) {
-      const int u = sl + G * k;
-      if (u < U) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t kk = ((mv[k] >> (8 * j)) & 0xffu)
-                                  ? (((rv[k] >> (8 * j)) & 0xffu) << 8) | (uint32_t)(4 * u + j)
-                                  : 0xffffu;
-          key = kk < key ? kk : key;
-        }
-      }
-    }
-    key = grp_reduce<G>(key, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
-    bi = (key >> 8) >= 255u ? 0 : (int)(key & 0xffu);
-    a_raw = bi;
-  } else if constexpr (CLOSEST) {
+  if constexpr (CLOSEST) {
     float best = __builtin_inff();
 #pragma unroll
     for (int k = 0; k < KU; ++k) {
@@ -501,65 +476,6 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
     done[b] = it == (int64_t)(P - 1);
     i_out[b] = it + 1;
     reward[b] = 0;
-  }
-}
-
-// co_slap_closest_rank: rank[b, j] = the position of location j in the instance's order
-// by (depot distance, index) -- the closest-free bench policy's precomputation, once per
-// episode -- and 255 where the distance is not finite (NaN / +inf: never picked, as in
-// co_slap_closest_step).  16 lanes per instance; the instance's 40-bit keys (the
-// order-preserving u32 image of the distance, then the index) staged in its group's LDS
-// row; each lane counts, for each of its locations, the keys below it (one 64-bit
-// compare + carry add per pair).
-template <int KU>
-__global__ __launch_bounds__(256) void slap_closest_rank_kernel(int64_t B, int L,
-                                                                const float* __restrict__ dist,
-                                                                uint8_t* __restrict__ rank) {
-  constexpr int G = 16;
-  __shared__ uint64_t s_key[256 / G][256];
-  const int sl = threadIdx.x & (G - 1), grp = threadIdx.x / G;
-  const int64_t b = (int64_t)blockIdx.x * (256 / G) + grp;
-  const bool live = b < B;
-  const int64_t bb = live ? b : B - 1;
-  const int U = L >> 2;
-  const float4* drow = reinterpret_cast<const float4*>(dist + bb * (int64_t)L);
-  uint64_t key[KU][4];
-  bool fin[KU][4];
-#pragma unroll
-  for (int k = 0; k < KU; ++k) {
-    const int u = sl + G * k;
-    const float4 d = drow[u < U ? u : U - 1];
-    const float d4[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t bits = d4[j] == 0.f ? 0u : __float_as_uint(d4[j]);  // -0 ties +0
-      const uint32_t ord = bits ^ ((uint32_t)((int32_t)bits >> 31) | 0x80000000u);
-      fin[k][j] = d4[j] < __builtin_inff();
-      key[k][j] = ((uint64_t)(fin[k][j] ? ord : 0xffffffffu) << 8) | (uint64_t)(4 * u + j);
-      if (u < U) s_key[grp][4 * u + j] = key[k][j];
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();  // a group's row is written and read by its own wave
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  uint32_t cnt[KU][4] = {};
-  for (int i = 0; i < L; i += 2) {
-    const uint64_t k0 = s_key[grp][i], k1 = s_key[grp][i + 1];
-#pragma unroll
-    for (int k = 0; k < KU; ++k)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cnt[k][j] += (uint32_t)(k0 < key[k][j]) + (uint32_t)(k1 < key[k][j]);
-  }
-  if (!live) return;
-  uint32_t* rrow = reinterpret_cast<uint32_t*>(rank + b * (int64_t)L);
-#pragma unroll
-  for (int k = 0; k < KU; ++k) {
-    const int u = sl + G * k;
-    if (u >= U) continue;
-    uint32_t w = 0u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) w |= (fin[k][j] ? cnt[k][j] : 255u) << (8 * j);
-    rrow[u] = w;
   }
 }
 
@@ -710,62 +626,6 @@ extern "C" int co_slap_closest_step(int64_t B, int64_t L, int64_t P, const float
   return launch_status();
 }
 
-
-extern "C" int co_slap_closest_rank(int64_t B, int64_t L, const float* dist, uint8_t* rank,
-                                    void* stream) {
-  if (B < 0 || L <= 0) return CO_E_INVAL;
-  if (B == 0) return CO_OK;
-  if (!dist || !rank) return CO_E_INVAL;
-  if (L % 4 != 0 || L > 252) return CO_E_INVAL;
-  if ((reinterpret_cast<uintptr_t>(dist) & 15) || (reinterpret_cast<uintptr_t>(rank) & 3))
-    return CO_E_ALIGN;
-  const dim3 grid((unsigned)((B + 15) / 16));
-  const int ku = (int)((L / 4 + 15) / 16);
-#define CO_SLAP_RK(K)                                                                         \
-  hipLaunchKernelGGL(slap_closest_rank_kernel<K>, grid, dim3(256), 0, (hipStream_t)stream, B, \
-                     (int)L, dist, rank)
-  switch (ku) {
-    case 1: CO_SLAP_RK(1); break;
-    case 2: CO_SLAP_RK(2); break;
-    case 3: CO_SLAP_RK(3); break;
-    default: CO_SLAP_RK(4);
-  }
-#undef CO_SLAP_RK
-  return launch_status();
-}
-
-extern "C" int co_slap_closest_step_ranked(int64_t B, int64_t L, int64_t P, const uint8_t* rank,
-                                           const float* to_choose, int64_t tc_stride,
-                                           const int32_t* assign_in, int32_t* assign,
-                                           const uint8_t* mask_in, uint8_t* mask_out,
-                                           int64_t* action_out, const int64_t* i_in,
-                                           int64_t* i_out, uint8_t* done, uint8_t* reward,
-                                           int32_t* status, void* stream) {
-  if (B < 0 || L <= 0 || P <= 0) return CO_E_INVAL;
-  if (B == 0) return CO_OK;
-  if (!rank || !to_choose || !assign_in || !assign || !mask_in || !mask_out || !action_out ||
-      !i_in || !i_out || !done || !reward)
-    return CO_E_INVAL;
-  if (L % 4 != 0 || L > 252) return CO_E_INVAL;
-  if ((reinterpret_cast<uintptr_t>(rank) | reinterpret_cast<uintptr_t>(mask_in) |
-       reinterpret_cast<uintptr_t>(mask_out)) & 3)
-    return CO_E_ALIGN;
-  const dim3 grid((unsigned)((B + 15) / 16));
-  const int ku = (int)((L / 4 + 15) / 16);
-#define CO_SLAP_RS(K)                                                                          \
-  hipLaunchKernelGGL((slap_closest_step_kernel<K, true, true>), grid, dim3(256), 0,            \
-                     (hipStream_t)stream, B, (int)L, (int)P, reinterpret_cast<const float*>(rank), \
-                     mask_in, mask_out, nullptr, action_out, to_choose, tc_stride, assign_in,   \
-                     assign, i_in, i_out, done, reward, status)
-  switch (ku) {
-    case 1: CO_SLAP_RS(1); break;
-    case 2: CO_SLAP_RS(2); break;
-    case 3: CO_SLAP_RS(3); break;
-    default: CO_SLAP_RS(4);
-  }
-#undef CO_SLAP_RS
-  return launch_status();
-}
 
 // ---------------------------------------------------------------- instance generator
 // The deterministic part of SLAPGenerator._generate (slap/generator.py:51-81,137-155) on

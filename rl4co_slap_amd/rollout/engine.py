@@ -111,18 +111,13 @@ class SLAPStepwiseEpisode(_GraphEpisode):
     closest-free bench policy each step is one co_slap_closest_step launch (policy +
     step), teacher-forced actions go through co_slap_step alone."""
 
-    def __init__(self, td, actions=None, policy: str = "teacher", ranked: bool = True):
+    def __init__(self, td, actions=None, policy: str = "teacher"):
         locs = td["locs"]
         super().__init__(locs.device)
         d = locs.device
         b, l = locs.shape[0], locs.shape[1]
         p = td["freq"].shape[-2]
         self.b, self.l, self.p, self.policy = b, l, p, policy
-        # the closest-free policy from per-episode ranks (co_slap_closest_rank: L bytes per
-        # step instead of 4L of distances) where the slot count allows it
-        self.ranked = (policy == "closest" and ranked and l % 4 == 0 and l <= 252
-                       and td["depot_loc_dist"].contiguous().data_ptr() % 16 == 0)
-        self.rank = torch.empty((b, l), dtype=torch.uint8, device=d) if self.ranked else None
         self.locs = locs.contiguous()
         self.picklist = td["picklist"].contiguous()
         self.depot_dist = td["depot_loc_dist"].contiguous()
@@ -146,8 +141,6 @@ class SLAPStepwiseEpisode(_GraphEpisode):
         b, l, p = self.b, self.l, self.p
         nat.call("co_slap_reset", b, l, p, nat.ptr(self.mask[0]), nat.ptr(self.to_choose),
                  nat.ptr(self.i[0]), nat.ptr(self.reset_reward), nat.ptr(self.ratio), s)
-        if self.ranked:
-            nat.call("co_slap_closest_rank", b, l, nat.ptr(self.depot_dist), nat.ptr(self.rank), s)
         for t in range(p):
             src, dst = t & 1, (t + 1) & 1
             a = self.acts[t]
@@ -156,13 +149,6 @@ class SLAPStepwiseEpisode(_GraphEpisode):
             # writes out of place from it (the reference clones, slap/env.py:50), later ones
             # in place
             a_in = self.assign0 if t == 0 else self.assign
-            if self.ranked:  # the bench policy (ranks) fused with the step: one launch
-                nat.call("co_slap_closest_step_ranked", b, l, p, nat.ptr(self.rank), nat.ptr(tc), p,
-                         nat.ptr(a_in), nat.ptr(self.assign), nat.ptr(self.mask[src]),
-                         nat.ptr(self.mask[dst]),
-                         nat.ptr(a), nat.ptr(self.i[src]), nat.ptr(self.i[dst]),
-                         nat.ptr(self.done), nat.ptr(self.step_reward), nat.ptr(self.status), s)
-                continue
             if self.policy == "closest":  # the bench policy fused with the step: one launch
                 nat.call("co_slap_closest_step", b, l, p, nat.ptr(self.depot_dist), nat.ptr(tc), p,
                          nat.ptr(a_in), nat.ptr(self.assign), nat.ptr(self.mask[src]),

@@ -199,17 +199,14 @@ def test_slap_rollout_matches_oracle(dev, cls_name, b, policy):
                                                       (10, 10, 20, 20), (4, 5, 19, 7),
                                                       (7, 7, 20, 9)])
 @pytest.mark.parametrize("dist", ["grid", "random_ties", "zeros_inf"])
-@pytest.mark.parametrize("cls_name", ["SLAPFusedEpisode", "SLAPStepwiseEpisode",
-                                      "SLAPStepwiseEpisode:dist"])
+@pytest.mark.parametrize("cls_name", ["SLAPFusedEpisode", "SLAPStepwiseEpisode"])
 def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist, cls_name):
     """Closest-free episodes for every lane-group width of the fused kernel (L = 48 -> 8
     lanes, 100 -> 16, 180 -> 32), P close to L - 1 (a lane's sorted list runs dry), and
     depot distances with many exact ties at random positions; the stepwise engine's
     co_slap_closest_step (policy + step in one launch: 1 / 2 / 3 units of 4 locations
-    per lane; L = 49 takes its two-launch fallback) -- by default from the per-episode ranks
-    of co_slap_closest_rank (co_slap_closest_step_ranked), ":dist" from the distances.
-    "zeros_inf": ties of -0.0 / +0.0 and a few +inf distances (never picked while a finite
-    free slot is left)."""
+    per lane; L = 49 takes its two-launch fallback).  "zeros_inf": ties of -0.0 / +0.0 and
+    a few +inf distances (never picked while a finite free slot is left)."""
     import numpy as np
 
     import rl4co_slap_amd.rollout.engine as eng
@@ -232,12 +229,8 @@ def test_slap_fused_closest_sizes(dev, aisles, locs, prods, orders, dist, cls_na
         dd[sel > 0.97] = float("inf")
     td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
     r, tdf, a = ref_rollout(env, td, slap_closest_free_action)
-    kw = {"ranked": False} if cls_name.endswith(":dist") else {}
-    ep = getattr(eng, cls_name.split(":")[0])(
-        TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev), None, policy="closest",
-        **kw)
-    if cls_name == "SLAPStepwiseEpisode":
-        assert ep.ranked == (aisles * locs % 4 == 0)
+    ep = getattr(eng, cls_name)(TensorDict({k: v.clone() for k, v in gen.items()}, [b]).to(dev),
+                                None, policy="closest")
     ep.run_eager()
     torch.cuda.synchronize()
     assert int(ep.status.item()) == 0
