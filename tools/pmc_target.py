@@ -36,8 +36,9 @@ elif args.kernel.startswith("cvrp"):
           "locs": locs_all[:, 1:].contiguous().to(dev), "demand": demand.to(dev)}
     if args.kernel == "cvrp_fused_nearest":
         ep = engine.CVRPFusedEpisode(td)
-    else:  # cvrp_stepwise: the graph-chunked reference loop (replay = one episode)
-        ep = engine.CVRPStepwiseEpisode(td).capture()
+    else:  # cvrp_stepwise[_pair]: the graph-chunked reference loop (replay = one episode);
+        # _pair: the policy and co_cvrp_step as two launches (the env step kernel alone)
+        ep = engine.CVRPStepwiseEpisode(td, fused_policy=not args.kernel.endswith("_pair")).capture()
         ep.run_eager = ep.replay
 elif args.kernel == "pomo_tsp100":
     from rl4co_slap_amd.rollout.pomo import POMOEpisode
