@@ -376,6 +376,14 @@ int co_distance_matrix(int64_t batch, int64_t num_loc, const float* locs, float*
 /* Number of rows with done[b] == 0 written to *count (device int32). */
 int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream);
 
+/* *out (device int32) = max(0, max over rows b of (width - sum of rows[b*row_stride + c],
+ * c < width)).  The decode loop's `while not td["done"].all()` poll for CVRP
+ * (constructive/base.py:245, cvrp/env.py:92 done = visited.sum(-1) == N+1): a positive
+ * deficit d means no instance set can be all done within the next d - 1 steps, so those
+ * host syncs are skipped without changing the stopping step. */
+int co_row_deficit_max(const uint8_t* rows, int64_t n_rows, int64_t width, int64_t row_stride,
+                       int32_t* out, void* stream);
+
 /* Device instance generation for throughput runs: the Uniform
  * samplers of tsp/generator.py:51-60 and cvrp/generator.py:116-143 on a Philox-4x32-10
  * stream (key = seed, block counter offset + i/4) instead of torch's CPU generator, so the

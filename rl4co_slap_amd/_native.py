@@ -51,6 +51,7 @@ _SIGS = {
     "co_slap_closest_step": [_i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p,
                              _p, _p],
     "co_count_not_done": [_p, _i64, _p, _p],
+    "co_row_deficit_max": [_p, _i64, _i64, _i64, _p, _p],
     "co_probe_copy": [_p, _p, _i64, _p],
     "co_uniform_fill": [_p, _i64, _f32, _f32, _f32, _i32, _u64, _u64, _p],
     "co_randint_fill": [_p, _i64, _i64, _i64, _u64, _u64, _p],

@@ -170,6 +170,37 @@ extern "C" int co_any_eq_i64(const int64_t* x, int64_t n, int64_t value, int32_t
   return launch_status();
 }
 
+// co_row_deficit_max: out = max(0, max_b(width - sum of row b's bytes)), a wave per row
+// (grid-stride), one atomicMax per wave with a positive deficit.  The decode loop's done
+// poll for CVRP: a row whose visited bytes sum to width - d cannot be done within d - 1
+// more steps (a step adds at most one to the sum), so the loop skips those polls.
+__global__ __launch_bounds__(256) void row_deficit_kernel(const uint8_t* __restrict__ rows,
+                                                          int64_t n_rows, int width,
+                                                          int64_t stride, int32_t* out) {
+  const int lane = lane_id();
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int best = 0;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n_rows; r += nw) {
+    const uint8_t* row = rows + r * stride;
+    int sum = 0;
+    for (int c = lane; c < width; c += 64) sum += row[c];
+    sum = wave_sum(sum);
+    best = max(best, width - sum);
+  }
+  if (lane == 0 && best > 0) atomicMax(out, best);
+}
+
+extern "C" int co_row_deficit_max(const uint8_t* rows, int64_t n_rows, int64_t width,
+                                  int64_t row_stride, int32_t* out, void* stream) {
+  if (n_rows < 0 || width <= 0 || width > (1 << 24) || !out || (n_rows > 0 && !rows))
+    return CO_E_INVAL;
+  int rc = zero_i32(out, (hipStream_t)stream);
+  if (rc != 0 || n_rows == 0) return rc == 0 ? CO_OK : rc;
+  hipLaunchKernelGGL(row_deficit_kernel, dim3(grid_for(n_rows, 4, 256 * 8)), dim3(256), 0,
+                     (hipStream_t)stream, rows, n_rows, (int)width, row_stride, out);
+  return launch_status();
+}
+
 extern "C" int co_count_not_done(const uint8_t* done, int64_t n, int32_t* count, void* stream) {
   if (n < 0 || !count || (n > 0 && !done)) return CO_E_INVAL;
   hipLaunchKernelGGL(count_not_done_kernel, dim3(1), dim3(kReduceThreads), 0,

@@ -240,6 +240,13 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
             return None
         return rec[1]
 
+    def poll_done(self, td):
+        """The decode loop's ``td["done"].all()`` (``constructive/base.py:245``), read on
+        the host: ``(all_done, k)``; when not all done, the next ``k - 1`` steps cannot
+        make every instance done either, so the loop polls again after ``k`` steps (the
+        same stopping step; fewer host syncs).  Default: ``k = 1``."""
+        return bool(td["done"].all()), 1
+
     def min_steps_to_done(self, td) -> int:
         """A host-side lower bound on the env steps still needed before every instance
         of ``td`` can be done (0 = unknown: poll).  The decode loop skips the

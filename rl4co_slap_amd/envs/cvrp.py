@@ -149,6 +149,24 @@ class CVRPEnv(RL4COEnvBase):
                       "reward": reward, "done": done, "action_mask": mask})
         return td
 
+    def poll_done(self, td):
+        """``done = visited.sum(-1) == N+1`` (``cvrp/env.py:92``) and a step adds at most one
+        to a row's sum: the largest row deficit d (``co_row_deficit_max``, one device read
+        like ``done.all()``) means no instance set is all done for d - 1 more steps."""
+        vis = td["visited"]
+        if vis.device.type != "cuda" or vis.dim() != 2 or vis.stride(1) != 1 \
+                or vis.dtype != torch.uint8:
+            return super().poll_done(td)
+        w = getattr(self, "_deficit_word", None)
+        if w is None or w.device != vis.device:
+            w = self._deficit_word = torch.zeros(1, dtype=torch.int32, device=vis.device)
+        nat.call("co_row_deficit_max", nat.ptr(vis), vis.shape[0], vis.shape[1], vis.stride(0),
+                 nat.ptr(w), nat.stream_of(vis))
+        d = int(w.item())
+        if d >= 1:
+            return False, d
+        return bool(td["done"].all()), 1
+
     def min_steps_to_done(self, td) -> int:
         """done = every node incl. the depot visited; a step visits one node."""
         return self._known_lb(td.get_raw("visited") if hasattr(td, "get_raw")

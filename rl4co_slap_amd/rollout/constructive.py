@@ -129,7 +129,13 @@ class ConstructivePolicy(nn.Module):
             td, env, hidden = hook(td, env, hidden, num_starts)
         step = 0
         decode = _direct_call(self.decoder)
-        while step < lb or not td["done"].all():
+        poll = getattr(env, "poll_done", None) or (lambda t: (bool(t["done"].all()), 1))
+        while True:
+            if step >= lb:  # the reference's `while not td["done"].all()` test
+                done, k = poll(td)
+                if done:
+                    break
+                lb = step + k  # cannot be all done before then: no host sync until
             logits, mask = decode(td, hidden, num_starts)
             act = actions[..., step] if actions is not None else None
             # decode + env step as one launch where the env provides it (TSP), else both

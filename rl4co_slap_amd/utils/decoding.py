@@ -135,7 +135,13 @@ def rollout(env, td, policy, max_steps: int = None):
     max_steps = float("inf") if max_steps is None else max_steps
     actions, steps = [], 0
     lb = env.min_steps_to_done(td) if hasattr(env, "min_steps_to_done") else 0
-    while steps < lb or not td["done"].all():  # same stop; polls only once it can be done
+    poll = getattr(env, "poll_done", None) or (lambda t: (bool(t["done"].all()), 1))
+    while True:  # same stop; polls only once every instance can be done
+        if steps >= lb:
+            done, k = poll(td)
+            if done:
+                break
+            lb = steps + k
         td = policy(td)
         actions.append(td["action"])
         td = env.step(td)["next"]

@@ -102,9 +102,35 @@ def test_loop_stops_on_the_reference_step(dev, name):
     tdev = table.to(dev)
     from rl4co_slap_amd.rollout import LogitsDecoder
     pol = ConstructivePolicy(None, LogitsDecoder(lambda t: tdev[next(it)]), env_name=name)
+    polls = []
+    real_poll = env.poll_done
+    env.poll_done = lambda t: polls.append(1) or real_poll(t)
     out = pol(td, env, phase="test", decode_type="greedy", return_actions=True)
     assert out["actions"].shape == ref["actions"].shape
     assert torch.equal(out["actions"].cpu(), ref["actions"])
+    steps = out["actions"].shape[1]
+    # polls start at the reset's bound (n / n+1 steps); CVRP's row-deficit poll skips the
+    # steps that cannot finish every instance
+    assert len(polls) <= steps - (n if name == "tsp" else n + 1) + 1
+    if name == "cvrp" and steps > n + 4:
+        assert len(polls) < steps - n
+
+
+def test_cvrp_row_deficit_poll_kernel(dev):
+    from rl4co_slap_amd import _native as nat
+
+    g = torch.Generator().manual_seed(4)
+    for b, w, pad in [(1, 5, 0), (37, 101, 0), (300, 101, 3), (64, 17, 1), (5, 600, 0)]:
+        base = (torch.rand(b, w + pad, generator=g) < 0.9).to(torch.uint8)
+        base[b // 2, :w] = 1  # a finished row
+        if b > 3:
+            base[1, 0] = 3  # a byte above 1 counts with its value, as visited.sum(-1)
+        x = base.to(dev)[:, :w]  # row stride w + pad
+        out = torch.full((1,), 77, dtype=torch.int32, device=dev)
+        nat.call("co_row_deficit_max", nat.ptr(x), b, w, x.stride(0), nat.ptr(out),
+                 nat.stream_of(x))
+        ref = max(0, int((w - base[:, :w].int().sum(1)).max()))
+        assert int(out.item()) == ref, (b, w, pad)
 
 
 def test_batchify_is_zero_copy_until_read(dev):
