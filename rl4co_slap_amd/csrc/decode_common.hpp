@@ -396,8 +396,11 @@ struct DecodeRow {  // OPT: clip / temperature flags as in GreedyRow::softmax_sh
 // DecodeRow, so actions and logp are the bits DecodeRow produces.  A row whose L is not
 // finite (every action masked, a NaN / +inf logit) has NaN log-probabilities throughout:
 // index 0 (torch.argmax picks the first NaN), logp NaN.  The mask is kept as 4-byte
-// words (pad slots past N read as masked).  VW = elements per load: 4 (float4 + u32 mask,
-// N % 4 == 0), 2 (float2 + u16, N even) or 1.
+// words (pad slots past N read as masked).  VW = 4: float4 + u32 mask loads on 16-byte /
+// 4-byte aligned rows (N % 4 == 0); VW = 3: the same 4-element chunks on rows of any N
+// (logits rows 4-byte aligned, mask rows byte aligned: gfx950 takes dword-aligned
+// dwordx4 and byte-aligned dword global accesses), the row's last partial chunk element
+// by element.
 template <int VW>
 struct Chunk;
 template <>
@@ -405,15 +408,12 @@ struct Chunk<4> {
   using F = float4;
   using M = uint32_t;
 };
+typedef float f4_align4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32_align1 __attribute__((aligned(1)));
 template <>
-struct Chunk<2> {
-  using F = float2;
-  using M = uint16_t;
-};
-template <>
-struct Chunk<1> {
-  using F = float;
-  using M = uint8_t;
+struct Chunk<3> {
+  using F = f4_align4;
+  using M = u32_align1;
 };
 
 template <int RL, int EPL, int VW>
@@ -428,24 +428,27 @@ struct GreedyRow {
     using M = typename Chunk<VW>::M;
 #pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {
-      uint32_t mm = 0u;
+      const int c = c0 + 4 * j;
+      uint32_t m = 0u;
+      float xf[4] = {0.f, 0.f, 0.f, 0.f};
+      if (valid && c + 4 <= N) {
+        const F x = *reinterpret_cast<const F*>(lrow + c);
+        xf[0] = x[0];
+        xf[1] = x[1];
+        xf[2] = x[2];
+        xf[3] = x[3];
+        m = mrow ? (uint32_t) * reinterpret_cast<const M*>(mrow + c) : 0x01010101u;
+      } else if (VW == 3 && valid && c < N) {  // the row's partial last chunk
 #pragma unroll
-      for (int h = 0; h < 4 / VW; ++h) {
-        const int c = c0 + 4 * j + VW * h;
-        F x;
-        uint32_t m = 0u;
-        if (valid && c < N) {
-          x = *reinterpret_cast<const F*>(lrow + c);
-          m = mrow ? (uint32_t) * reinterpret_cast<const M*>(mrow + c) : (0x01010101u >> (32 - 8 * VW));
-        } else {
-          x = F{};
-        }
-        const float* xf = reinterpret_cast<const float*>(&x);
-#pragma unroll
-        for (int q = 0; q < VW; ++q) v[4 * j + VW * h + q] = xf[q];
-        mm |= m << (8 * VW * h);
+        for (int q = 0; q < 3; ++q)
+          if (c + q < N) {
+            xf[q] = lrow[c + q];
+            m |= (mrow ? (uint32_t)mrow[c + q] : 1u) << (8 * q);
+          }
       }
-      mw[j] = mm;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[4 * j + q] = xf[q];
+      mw[j] = m;
     }
   }
 
@@ -453,28 +456,35 @@ struct GreedyRow {
   __device__ __forceinline__ void store_mask(int N, uint8_t* orow, int c0) const {
     using M = typename Chunk<VW>::M;
 #pragma unroll
-    for (int j = 0; j < EPL / 4; ++j)
+    for (int j = 0; j < EPL / 4; ++j) {
+      const int c = c0 + 4 * j;
+      if (c + 4 <= N) {
+        *reinterpret_cast<M*>(orow + c) = (M)mw[j];
+      } else if (VW == 3 && c < N) {
 #pragma unroll
-      for (int h = 0; h < 4 / VW; ++h) {
-        const int c = c0 + 4 * j + VW * h;
-        if (c < N) *reinterpret_cast<M*>(orow + c) = (M)(mw[j] >> (8 * VW * h));
+        for (int q = 0; q < 3; ++q)
+          if (c + q < N) orow[c + q] = (uint8_t)(mw[j] >> (8 * q));
       }
+    }
   }
   __device__ __forceinline__ void store_logp(int N, float L, float* frow, int c0) const {
     using F = typename Chunk<VW>::F;
 #pragma unroll
-    for (int j = 0; j < EPL / 4; ++j)
+    for (int j = 0; j < EPL / 4; ++j) {
+      const int c = c0 + 4 * j;
+      if (c + 4 <= N) {
+        F x;
+        x[0] = v[4 * j] - L;
+        x[1] = v[4 * j + 1] - L;
+        x[2] = v[4 * j + 2] - L;
+        x[3] = v[4 * j + 3] - L;
+        *reinterpret_cast<F*>(frow + c) = x;
+      } else if (VW == 3 && c < N) {
 #pragma unroll
-      for (int h = 0; h < 4 / VW; ++h) {
-        const int c = c0 + 4 * j + VW * h;
-        if (c < N) {
-          F x;
-          float* xf = reinterpret_cast<float*>(&x);
-#pragma unroll
-          for (int q = 0; q < VW; ++q) xf[q] = v[4 * j + VW * h + q] - L;
-          *reinterpret_cast<F*>(frow + c) = x;
-        }
+        for (int q = 0; q < 3; ++q)
+          if (c + q < N) frow[c + q] = v[4 * j + q] - L;
       }
+    }
   }
 
   __device__ __forceinline__ bool allowed(int k) const {
@@ -1062,8 +1072,7 @@ inline int greedy_vw(int64_t N, int64_t lstride, const float* logits, const uint
   const uintptr_t f = reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(full);
   const uintptr_t m = reinterpret_cast<uintptr_t>(m_in) | reinterpret_cast<uintptr_t>(m_out);
   if (N % 4 == 0 && lstride % 4 == 0 && (f & 15) == 0 && (m & 3) == 0) return 4;
-  if (N % 2 == 0 && lstride % 2 == 0 && (f & 7) == 0 && (m & 1) == 0) return 2;
-  return 1;
+  return 3;  // 4-element chunks on rows of any N and alignment
 }
 
 inline bool decode_vec_ok(const float* logits, int64_t lstride, const uint8_t* mask, int64_t N) {

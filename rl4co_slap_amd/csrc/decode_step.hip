@@ -51,8 +51,7 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
                   logp_sel, full, status)
     switch (greedy_vw(N, lstride, logits, mask, mask, full)) {
       case 4: CO_ROW_DISPATCH(CO_GREEDY, 4); break;
-      case 2: CO_ROW_DISPATCH(CO_GREEDY, 2); break;
-      default: CO_ROW_DISPATCH(CO_GREEDY, 1);
+      default: CO_ROW_DISPATCH(CO_GREEDY, 3);
     }
 #undef CO_GREEDY
     return launch_status();

@@ -30,8 +30,7 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
                   ll_accum, status)
     switch (greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr)) {
       case 4: CO_ROW_DISPATCH(CO_TDG, 4); break;
-      case 2: CO_ROW_DISPATCH(CO_TDG, 2); break;
-      default: CO_ROW_DISPATCH(CO_TDG, 1);
+      default: CO_ROW_DISPATCH(CO_TDG, 3);
     }
 #undef CO_TDG
     return launch_status();
