@@ -10,6 +10,8 @@ import bench  # noqa: E402
 from rl4co_slap_amd import _native as nat  # noqa: E402
 
 d = torch.device("cuda:0")
+if os.environ.get("CO_LIB"):  # a variant library (tools/build_variants.sh)
+    nat.LIB_PATH = os.environ["CO_LIB"]
 nat.load()
 b, n = 32768, 100
 act = torch.randint(0, n + 1, (b,), device=d)
