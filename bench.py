@@ -493,6 +493,9 @@ def main():
         # per step, Python TensorDict plumbing)
         modes["dropin_tsp100"] = bench_dropin(b, n, k, world, rank, dev)
         modes["dropin_cvrp100"] = bench_dropin_cvrp(32768, 100, k, world, rank, dev)
+        # the fork's SLAP policy path (examples/slap.py): config 4's batch and the north star's
+        modes["dropin_slap_b16384"] = bench_dropin_slap(args.slap_batch, k, world, rank, dev)
+        modes["dropin_slap_b65536"] = bench_dropin_slap(65536, k, world, rank, dev)
         # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
         modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
         # the north star's "SLAP at batch 65,536": fused and stepwise
@@ -584,7 +587,12 @@ def annotate_modes(modes, n, world):
         "tsp_stepwise_graph": lambda m: 2 * n + 50 + (16 * n + 4) / n,
         "dropin_tsp100": lambda m: 2 * n + 50 + 5 * n + 16 + (16 * n + 4) / n,
         # decode: logits + mask read, action + logp written; the CVRP step as stepwise
-        "dropin_cvrp100": lambda m: 5 * (n + 1) + 12 + 16 * n + 50,
+        # the decode-fused CVRP step: logits 4(N+1) + mask N+1 read, logp out (the action
+        # written instead of read), the env step's 7N+33 + the episode reward
+        "dropin_cvrp100": lambda m: 5 * (n + 1) + 4 + 7 * n + 33 + (16 * m["episode_steps"] + 12)
+        / m["episode_steps"],
+        "dropin_slap_b16384": lambda m: 234 + 404 + 1684 / 20,
+        "dropin_slap_b65536": lambda m: 234 + 404 + 1684 / 20,
         "tsp_fused_nearest": lambda m: (17 * n + 30) / n,
         "slap_fused_closest": lambda m: 2754 / 20,
         "slap_fused_closest_b65536": lambda m: 2754 / 20,
@@ -819,7 +827,9 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
         logits = torch.randn(bb, n + 1, generator=g).to(dev)
         env = CVRPEnv(generator_params=dict(num_loc=n), device=dev)
         pol = ConstructivePolicy(None, LogitsDecoder(lambda td: logits), env_name="cvrp")
-        steps = []
+        steps, calls = [], []
+        real = env.decode_and_step
+        env.decode_and_step = lambda *a, **kw: calls.append(1) or real(*a, **kw)
 
         def run():
             td = env.reset(TensorDict(dict(data), [bb]))
@@ -834,12 +844,115 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
             out.update({"value": world * bb * T * kk / t, "ms_per_episode": t / kk * 1e3,
                         "gpu_ms_per_episode": ev / kk * 1e3, "episode_steps": T,
                         "gpu_us_per_step": ev / kk / T * 1e6, "batch_per_gpu": bb,
-                        "launches_per_step": 2,
-                        "path": "ConstructivePolicy.forward + CVRPEnv"})
+                        "launches_per_step": 1 if len(calls) == sum(steps) else 2,
+                        "path": "ConstructivePolicy.forward + CVRPEnv "
+                                "(co_cvrp_decode_step per step)"})
         else:
             out["host_us_per_step_b64"] = t / kk / T * 1e6
+        env.decode_and_step = real
     out["host_below_kernels"] = out["host_us_per_step_b64"] < out["gpu_us_per_step"]
     return out
+
+
+def bench_dropin_slap(b, k, world, rank, dev):
+    """The fork's own user path (examples/slap.py:74-93 -> constructive/base.py:229-251):
+    ``ConstructivePolicy.forward(td, SLAPEnv, greedy)`` on the config-4 instance recipe
+    (``examples/slap.py:75-76``: 10 aisles x 10 locations, 20 products / orders, 5 picks per
+    order; ``torch.manual_seed(1234 + rank)``, ``np.random.seed(1234 + rank)``), per step
+    the decode and the SLAP env step as ONE co_slap_decode_step launch (SLAPEnv.
+    decode_and_step), certified greedy with tanh clipping 10, P = 20 steps, then the pick-
+    tour reward and get_log_likelihood.  Decoders: a stub (a fixed HBM-resident [B, L]
+    logits tensor) and the SLAP pointer decoder of tests/am_pointer.py (examples/slap.py's
+    init embedding + zero context, glimpse + pointer over cached projections).  Beside
+    them: the host cost per loop step at B = 64 and the GPU time of the fused kernel at B."""
+    import numpy as np
+
+    from rl4co_slap_amd import _native
+    from rl4co_slap_amd.envs import SLAPEnv
+    from rl4co_slap_amd.envs.slap import SLAPGenerator
+    from rl4co_slap_amd.rollout.constructive import ConstructivePolicy, LogitsDecoder
+    from rl4co_slap_amd.td import TensorDict
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from am_pointer import SLAPPointerDecoder
+
+    out = {}
+    P = 20
+    for dec_name in ("stub", "am"):
+        for bb, kk in ((b, k), (64, 3 * k)):
+            torch.manual_seed(1234 + rank)
+            np.random.seed(1234 + rank)
+            data = SLAPGenerator(materialize_dist_mat=False)(bb).to(dev)
+            l = data["locs"].shape[1]
+            g = torch.Generator().manual_seed(11 + rank)
+            logits = torch.randn(bb, l, generator=g).to(dev)
+            env = SLAPEnv(device=dev)
+            dec = (LogitsDecoder(lambda td, lg=logits: lg) if dec_name == "stub"
+                   else SLAPPointerDecoder(data["locs"], dev))
+            pol = ConstructivePolicy(None, dec, env_name="slap", tanh_clipping=10.0)
+            calls = []
+            real = env.decode_and_step
+            env.decode_and_step = lambda *a, **kw: calls.append(1) or real(*a, **kw)
+
+            def run():
+                td = env.reset(TensorDict(dict(data.items()), [bb]))
+                return pol(td, env, phase="test", decode_type="greedy")
+
+            wall, ev = timed(run, kk, 2, world, dev)
+            t = max_over_ranks(wall, world, dev)
+            fused_steps = len(calls) / (kk + 2)
+            key = "" if dec_name == "stub" else "am_"
+            if bb == b:
+                m = {"value": world * bb * P * kk / t, "ms_per_episode": t / kk * 1e3,
+                     "gpu_ms_per_episode": ev / kk * 1e3,
+                     "launches_per_step": 1 if fused_steps == P else 2}
+                if dec_name == "stub":
+                    out.update(m)
+                    out.update({"batch_per_gpu": bb, "env_steps_per_episode": P,
+                                "done_polls_per_episode": 1,
+                                "path": "ConstructivePolicy.forward + SLAPEnv "
+                                        "(co_slap_decode_step per step)"})
+                else:
+                    out["am_decoder"] = m
+            else:
+                out[key + "host_us_per_step_b64"] = t / kk / P * 1e6
+            env.decode_and_step = real
+            del env, pol, dec, data
+    out["decode_fused_kernel_us"] = slap_decode_step_kernel_us(b, dev)
+    out["host_below_kernel"] = out["host_us_per_step_b64"] < out["decode_fused_kernel_us"]
+    # SURVEY 8d: the SLAP step 2L+34 B + the decode's logits 4L + logp 4 per env-step
+    out["bytes_per_env_step"] = 2 * 100 + 34 + 4 * 100 + 4
+    return out
+
+
+def slap_decode_step_kernel_us(b, dev, reps=50, l=100, p=20):
+    """GPU time of one co_slap_decode_step launch (certified greedy, clip 10, the drop-in
+    default) at B x L: a mid-episode state (10 products placed), out-of-place assignment,
+    HIP events over reps launches on the launching stream."""
+    from rl4co_slap_amd import _native
+
+    g = torch.Generator().manual_seed(5)
+    logits = torch.randn(b, l, generator=g).to(dev)
+    mask = (torch.rand(b, l, generator=g) < 0.9).to(dev)
+    mask[:, 0] = False
+    mask[:, 1] = True
+    tc = torch.arange(p, dtype=torch.float32).repeat(b, 1).to(dev)
+    asg = torch.randint(0, l, (b, p), dtype=torch.int32).to(dev)
+    i = torch.full((b, 1), p // 2, dtype=torch.int64, device=dev)
+    act = torch.empty(b, dtype=torch.int64, device=dev)
+    lp = torch.empty(b, dtype=torch.float32, device=dev)
+    asg_o, m_o = torch.empty_like(asg), torch.empty_like(mask)
+    i_o = torch.empty_like(i)
+    done, rw = (torch.empty((b, 1), dtype=torch.bool, device=dev) for _ in range(2))
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    launch = _native.bind("co_slap_decode_step", b, l, p, logits.data_ptr(), l, mask.data_ptr(),
+                          10.0, 1.0, _native.DECODE_CERTIFIED, None, act.data_ptr(),
+                          lp.data_ptr(), 0, 0, tc[:, p // 2:].data_ptr(), p, asg.data_ptr(),
+                          asg_o.data_ptr(), m_o.data_ptr(), i.data_ptr(), i_o.data_ptr(),
+                          done.data_ptr(), rw.data_ptr(), None, st.data_ptr())
+    _, ev = timed(lambda: launch(sh), reps, 5, 1, dev)
+    return ev / reps * 1e6
 
 
 def bench_cvrp(b, n, k, world, rank, dev):

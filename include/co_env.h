@@ -220,6 +220,40 @@ int co_tsp_decode_step(int64_t batch, int64_t num_loc, const float* logits,
                        uint8_t* done, uint8_t* step_reward, float* ll_accum, int32_t* status,
                        void* stream);
 
+/* co_decode_step fused with SLAPEnv._step (slap/env.py:38-93) for the selected action
+ * (replaces DecodingStrategy.step + env.step of constructive/base.py:245-251 on the fork's
+ * examples/slap.py policy path).  L = locations (the row length of logits / masks),
+ * P = products.  Decode as co_decode_step; then, with a = the selected action (evaluate:
+ * action_in, negative values index from the end as python indexing):
+ *   assign_out = assign_in with [b, (int)to_choose[b*tc_stride]] = (int)a (out of place:
+ *   the row is copied; in place: that element only); mask_out = mask_in minus a
+ *   (in-place NOT allowed); done[b] = i_in[b] == P-1; i_out = i_in + 1; step_reward = 0;
+ *   ll_accum (nullable) += logp_sel.  Same bits as co_decode_step + co_slap_step. */
+int co_slap_decode_step(int64_t batch, int64_t num_slots, int64_t n_products,
+                        const float* logits, int64_t logits_stride, const uint8_t* mask_in,
+                        float tanh_clipping, float temperature, int mode,
+                        const int64_t* action_in, int64_t* action_out, float* logp_sel,
+                        uint64_t seed, uint64_t offset, const float* to_choose,
+                        int64_t tc_stride, const int32_t* assign_in, int32_t* assign_out,
+                        uint8_t* mask_out, const int64_t* i_in, int64_t* i_out, uint8_t* done,
+                        uint8_t* step_reward, float* ll_accum, int32_t* status, void* stream);
+
+/* co_decode_step fused with CVRPEnv._step + get_action_mask (cvrp/env.py:73-149):
+ * N = customers, rows of logits / masks / visited are N+1 wide.  Decode as
+ * co_decode_step; then the co_cvrp_step transition for the selected action (evaluate:
+ * action_in): used_out, visited_out (separate buffer), current_out (nullable) = a,
+ * done, step_reward = 0, action_mask recomputed into mask_out (separate buffer);
+ * ll_accum (nullable) += logp_sel.  Same bits as co_decode_step + co_cvrp_step. */
+int co_cvrp_decode_step(int64_t batch, int64_t num_loc, const float* logits,
+                        int64_t logits_stride, const uint8_t* mask_in, float tanh_clipping,
+                        float temperature, int mode, const int64_t* action_in,
+                        int64_t* action_out, float* logp_sel, uint64_t seed, uint64_t offset,
+                        const float* demand, const float* used_in, float* used_out,
+                        const float* vehicle_capacity, const uint8_t* visited_in,
+                        uint8_t* visited_out, int64_t* current_out, uint8_t* done,
+                        uint8_t* step_reward, uint8_t* mask_out, float* ll_accum,
+                        int32_t* status, void* stream);
+
 /* ------------------------------------------- bench policies (in-kernel) */
 
 /* Deterministic cheap policies for the env-throughput benchmark

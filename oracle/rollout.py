@@ -49,7 +49,7 @@ def constructive_forward(td, env, logits_fn, decode_type="greedy", actions=None,
     if calc_reward:
         td["reward"] = env.get_reward(td, acts)
     return {"reward": td["reward"], "log_likelihood": get_log_likelihood(logprobs, acts, None),
-            "actions": acts}
+            "actions": acts, "td": td}
 
 
 def shared_baseline(reward, on_dim=1):

@@ -10,4 +10,20 @@ from . import _native
 from .envs import ENV_REGISTRY, CVRPEnv, SLAPEnv, TSPEnv, get_env
 from .td import TensorDict
 
-__all__ = ["ENV_REGISTRY", "CVRPEnv", "SLAPEnv", "TSPEnv", "get_env", "TensorDict", "_native"]
+
+def check_errors(device="cuda") -> None:
+    """Raise any error a device kernel without a caller-held status word recorded since
+    the last read (an out-of-range ``gather_by_index`` index, the analogue of torch.gather's
+    device-side assert).  The env's reward and ``post_decoder_hook`` read it with their own
+    status read; code that calls ``gather_by_index`` outside a decode loop / reward calls
+    this (one host sync) or runs with ``CO_SYNC_CHECKS=1`` (a read after every gather)."""
+    import torch
+
+    device = torch.device(device)
+    if device.type == "cuda" and device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    _native.check_deferred(device)
+
+
+__all__ = ["ENV_REGISTRY", "CVRPEnv", "SLAPEnv", "TSPEnv", "get_env", "TensorDict", "_native",
+           "check_errors"]

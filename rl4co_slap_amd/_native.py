@@ -58,6 +58,10 @@ _SIGS = {
     "co_pomo_shared_baseline": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
     "co_tsp_decode_step": [_i64, _i64, _p, _i64, _p, _f32, _f32, _i32, _p, _p, _p, _u64, _u64, _p,
                            _p, _p, _p, _p, _i32, _p, _p, _p, _p, _p],
+    "co_slap_decode_step": [_i64, _i64, _i64, _p, _i64, _p, _f32, _f32, _i32, _p, _p, _p, _u64,
+                            _u64, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
+    "co_cvrp_decode_step": [_i64, _i64, _p, _i64, _p, _f32, _f32, _i32, _p, _p, _p, _u64, _u64,
+                            _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "co_tsp_rollout": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
     "co_tsp_rollout_ex": [_i64, _i64, _p, _p, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _i32,
                           _p, _p],
@@ -305,6 +309,7 @@ class _TorchStep:
         self.tsp_step_td = bound(mod.tsp_step_td, "co_tsp_decode_step")
         self.decode_step = bound(mod.decode_step, "co_decode_step")
         self.cvrp_step = bound(mod.cvrp_step, "co_cvrp_step")
+        self.clear_pool = mod.clear_pool
 
 
 def torchstep():

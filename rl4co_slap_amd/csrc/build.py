@@ -18,6 +18,7 @@ ROOT = os.path.dirname(PKG)
 OUT_DIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(OUT_DIR, "libco_env.so")
 SOURCES = ["tsp.hip", "cvrp.hip", "slap.hip", "ops.hip", "decode_step.hip", "decode_tsp.hip",
+           "decode_env.hip",
            "rollout.hip",
            "nearest.hip"]
 HEADERS = ["co_common.hpp", "co_tile.hpp", "co_math.hpp", "decode_common.hpp"]

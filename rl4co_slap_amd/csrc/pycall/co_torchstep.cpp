@@ -88,25 +88,50 @@ c10::Storage new_storage(const c10::Device& dev, int64_t nbytes) {
   return at::empty({nbytes}, at::TensorOptions().dtype(at::kByte).device(dev)).storage();
 }
 
+// Reuse is keyed by (device, size, stream): a storage is handed out again only on the
+// stream its previous users' kernels were queued on (then stream order protects them, as
+// the caching allocator's own same-stream reuse does); on another stream a new storage is
+// allocated.  The pool holds at most kMax storages over all keys: a new key evicts the
+// least recently used free entry, so batch-size / N changes (a last partial batch, a
+// validation batch) do not accumulate memory out of torch.cuda.empty_cache's reach;
+// clear_pool() drops everything.
 struct StatePool {
-  static constexpr int kPerKey = 4;
+  static constexpr int kPerKey = 4, kMax = 16;
   struct Entry {
     c10::Device dev;
     int64_t nbytes;
+    void* stream;
     c10::Storage st;
+    uint64_t last;
   };
   std::vector<Entry> entries;
-  c10::Storage acquire(const c10::Device& dev, int64_t nbytes) {
+  uint64_t tick = 0;
+  c10::Storage acquire(const c10::Device& dev, int64_t nbytes, void* stream) {
+    ++tick;
     int same = 0;
     for (auto& e : entries) {
-      if (e.dev != dev || e.nbytes != nbytes) continue;
+      if (e.dev != dev || e.nbytes != nbytes || e.stream != stream) continue;
       ++same;
-      if (e.st.use_count() == 1) return e.st;
+      if (e.st.use_count() == 1) {
+        e.last = tick;
+        return e.st;
+      }
     }
     c10::Storage st = new_storage(dev, nbytes);
-    if (same < kPerKey) entries.push_back(Entry{dev, nbytes, st});
+    if (same < kPerKey) {
+      if ((int)entries.size() >= kMax) evict_lru();
+      if ((int)entries.size() < kMax) entries.push_back(Entry{dev, nbytes, stream, st, tick});
+    }
     return st;
   }
+  void evict_lru() {  // the least recently used entry nobody else refers to
+    int victim = -1;
+    for (int k = 0; k < (int)entries.size(); ++k)
+      if (entries[k].st.use_count() == 1 && (victim < 0 || entries[k].last < entries[victim].last))
+        victim = k;
+    if (victim >= 0) entries.erase(entries.begin() + victim);
+  }
+  void clear() { entries.clear(); }
 };
 
 struct Slab {
@@ -167,13 +192,13 @@ int tsp_launch(TspDecodeStep fn, const at::Tensor& logits, const at::Tensor& mas
   Carver c;
   const int64_t om = c.take(b * nl), oi = c.take(8 * b), of = c.take(8 * b), od = c.take(b),
                 orw = c.take(b);
-  const c10::Storage st = g_state.acquire(dev, c.off);
+  void* stream = current_stream(dev);
+  const c10::Storage st = g_state.acquire(dev, c.off, stream);
   out[2] = view_of(st, at::kBool, om, {b, nl});
   out[3] = view_of(st, at::kLong, oi, i.sizes());
   out[4] = view_of(st, at::kLong, of, {b});
   out[5] = view_of(st, at::kBool, od, {b});
   out[6] = view_of(st, at::kBool, orw, {b});
-  void* stream = current_stream(dev);
   int rc;
   Py_BEGIN_ALLOW_THREADS
   rc = fn(b, nl, logits.const_data_ptr<float>(), logits.stride(0),
@@ -424,14 +449,14 @@ PyObject* cvrp_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
     Carver c;
     const int64_t ou = c.take(4 * b), ov = c.take(b * (nl + 1)), oc = c.take(8 * b),
                   od = c.take(b), orw = c.take(b), om = c.take(b * (nl + 1));
-    const c10::Storage st = g_state.acquire(dev, c.off);
+    void* stream = current_stream(dev);
+    const c10::Storage st = g_state.acquire(dev, c.off, stream);
     at::Tensor used_out = view_of(st, at::kFloat, ou, used.sizes());
     at::Tensor visited_out = view_of(st, at::kByte, ov, visited.sizes());
     at::Tensor cur = view_of(st, at::kLong, oc, {b, 1});
     at::Tensor done = view_of(st, at::kBool, od, {b});
     at::Tensor reward = view_of(st, at::kBool, orw, {b});
     at::Tensor mask = view_of(st, at::kBool, om, {b, nl + 1});
-    void* stream = current_stream(dev);
     int rc;
     Py_BEGIN_ALLOW_THREADS
     rc = fn(b, nl, action.const_data_ptr<int64_t>(), demand.const_data_ptr<float>(),
@@ -450,7 +475,15 @@ PyObject* cvrp_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
   }
 }
 
+// clear_pool() -> None: drop every pooled state storage (tensors still held stay valid)
+PyObject* clear_pool(PyObject*, PyObject* const*, Py_ssize_t) {
+  g_state.clear();
+  Py_RETURN_NONE;
+}
+
 PyMethodDef methods[] = {
+    {"clear_pool", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(clear_pool)),
+     METH_FASTCALL, "drop the pooled step-state storages"},
     {"tsp_step_td", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(tsp_step_td)),
      METH_FASTCALL, "TSPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
     {"decode_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(decode_step)),

@@ -348,9 +348,11 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
 // Teacher-forced TSP episode on ROW-MAJOR actions [B, N] (element (b, t) at
 // acts[b*sb + t]: the reference's own [B, T] layout, ConstructivePolicy's `actions`):
 // G lanes per instance, lane sl owns the EPL consecutive steps t = sl*EPL + k.  Every
-// input is read as a contiguous row -- the instance's 8N bytes of actions in 16-byte
-// vectors, its 8N bytes of coordinates gathered within one row (whole lines, L2) -- and
-// nothing is staged in LDS, so all of B is in flight without tile rounds.  The visited set
+// input is read as a contiguous row: MODE 2 (the headline's) stages a wave's GPW action
+// rows and GPW coordinate rows by LDS-DMA as two contiguous blocks and reads steps and
+// coordinate gathers from LDS; MODE 0 / 1 read the instance's 8N bytes of actions from
+// memory (scalar / 16-byte vectors) and gather its coordinates within one row (whole
+// lines, L2).  One block of instances per wave, all of B in flight.  The visited set
 // is a per-group LDS bitmap (no-return ds_or per step); the actions are a permutation iff
 // all N bits are set after the N steps (and every action is in range).  Edge lengths in
 // f32 (hardware sqrt, <= 1 ulp; reward parity is 1e-5 relative): within a lane, to the
@@ -380,7 +382,9 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
     uint8_t* __restrict__ done_out, uint8_t* __restrict__ step_reward_out,
     float* __restrict__ reward_out, int check, int32_t* status) {
   constexpr int GPW = 64 / G;
-  constexpr bool VEC = MODE == 1, DMA = MODE == 2;
+  // 16-byte action pairs only when every lane's first step t0 = sl*EPL is even (the row
+  // base is 16-byte aligned): an odd EPL takes the scalar loads
+  constexpr bool VEC = MODE == 1 && EPL % 2 == 0, DMA = MODE == 2;
   __shared__ uint32_t s_bits[4][GPW][(G * EPL + 31) / 32];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_rows[];  // DMA: per wave
   constexpr int NWB = (G * EPL + 31) / 32;
@@ -918,7 +922,9 @@ int launch_tsp_rows(int64_t B, int64_t N, const float2* l2, int64_t LB, const in
   do {                                                                                         \
     const dim3 grid((unsigned)(((B + 64 / GG - 1) / (64 / GG) + 3) / 4)), block(256);          \
     const size_t dsh = 4 * tsp_rows_wave_bytes(64 / GG, (int)N);                               \
-    if (dma_ok && (LB == B || LB % (64 / GG) == 0) && dsh <= 64 * 1024)                        \
+    /* the static visited bitmaps come on top of the dynamic staging (64 KiB default) */       \
+    const size_t sbits = (size_t)4 * (64 / GG) * ((GG * EE + 31) / 32) * 4;                    \
+    if (dma_ok && (LB == B || LB % (64 / GG) == 0) && dsh + sbits <= 64 * 1024)                \
       hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 2, STATE>), grid, block, dsh, s, B,   \
                          (int)N, l2, LB, acts, sb, mask_out, first_out, cur_out, i_out,        \
                          done_out, step_reward_out, reward_out, check, status);                \

@@ -149,6 +149,48 @@ class CVRPEnv(RL4COEnvBase):
                       "reward": reward, "done": done, "action_mask": mask})
         return td
 
+    def decode_and_step(self, td, logits, mode, temperature, tanh_clipping, action_in, seed,
+                        offset, status, key="action"):
+        """``DecodingStrategy.step`` + ``_step`` (``decoding.py:327-369``,
+        ``cvrp/env.py:73-149``) in one ``co_cvrp_decode_step`` launch: the same selection,
+        log-probability, RNG use and state (used / vehicle capacity, visited, current node,
+        done, the recomputed action mask) as the two calls.  Returns ``(action, logp)``, or
+        None when it does not apply (CPU tensors, non-f32 logits, long rows)."""
+        mask, demand, used, vcap, visited = (td["action_mask"], td["demand"],
+                                             td["used_capacity"], td["vehicle_capacity"],
+                                             td["visited"])
+        dev = logits.device
+        if dev.type != "cuda" or any(x.device != dev for x in (mask, demand, used, vcap, visited)):
+            return None
+        if logits.dtype != torch.float32 or logits.dim() != 2 or logits.stride(-1) != 1:
+            return None
+        b, n = demand.shape
+        if (logits.shape != (b, n + 1) or mask.shape != (b, n + 1) or n + 1 > 2048
+                or visited.dtype != torch.uint8 or demand.dtype != torch.float32
+                or used.dtype != torch.float32 or vcap.dtype != torch.float32
+                or used.numel() != b or vcap.numel() != b):
+            return None
+        m, demand, used, vcap, visited = (x.contiguous() for x in (mask, demand, used, vcap, visited))
+        ain = action_in.long().contiguous() if action_in is not None else None
+        s = nat.stream_of(m)
+        act = torch.empty(b, dtype=torch.int64, device=dev)  # kept by the strategy
+        logp = torch.empty(b, dtype=torch.float32, device=dev)
+        used_out = self._out(used.shape, used.dtype, dev, s)
+        visited_out = self._out(visited.shape, visited.dtype, dev, s)
+        cur = self._out((b, 1), torch.int64, dev, s)
+        done = self._out((b,), torch.bool, dev, s)
+        reward = self._out((b,), torch.bool, dev, s)
+        mask_out = self._out((b, n + 1), torch.bool, dev, s)
+        nat.call("co_cvrp_decode_step", b, n, nat.ptr(logits), logits.stride(0), nat.ptr(m),
+                 float(tanh_clipping), float(temperature), mode, nat.ptr(ain), nat.ptr(act),
+                 nat.ptr(logp), seed, offset, nat.ptr(demand), nat.ptr(used), nat.ptr(used_out),
+                 nat.ptr(vcap), nat.ptr(visited), nat.ptr(visited_out), nat.ptr(cur),
+                 nat.ptr(done), nat.ptr(reward), nat.ptr(mask_out), None, nat.ptr(status), s)
+        sel = action_in if action_in is not None else act
+        set_many(td, {key: sel})
+        self._after_step(td, used_out, visited_out, cur, done, reward, mask_out)
+        return sel, logp
+
     def poll_done(self, td):
         """``done = visited.sum(-1) == N+1`` (``cvrp/env.py:92``) and a step adds at most one
         to a row's sum: the largest row deficit d (``co_row_deficit_max``, one device read

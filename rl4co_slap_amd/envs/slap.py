@@ -6,7 +6,7 @@ import numpy as np
 import torch
 
 from .. import _native as nat
-from ..td import TensorDict
+from ..td import TensorDict, set_many
 from .base import RL4COEnvBase
 from .common import Generator, device_uniform
 
@@ -162,6 +162,49 @@ class SLAPEnv(RL4COEnvBase):
         td.update({"assignment": assign_out, "to_choose": tc[..., 1:], "action_mask": mask_out,
                    "i": i_out, "reward": reward, "done": done})
         return td
+
+    def decode_and_step(self, td, logits, mode, temperature, tanh_clipping, action_in, seed,
+                        offset, status, key="action"):
+        """``DecodingStrategy.step`` + ``_step`` (``decoding.py:327-369``,
+        ``slap/env.py:38-93``) in one ``co_slap_decode_step`` launch: the same selection,
+        log-probability, RNG use and state (assignment row written out of place, the
+        mask minus the action, ``done = i == P-1``, ``to_choose`` shrunk as a view) as the
+        two calls.  Returns ``(action, logp)``, or None when it does not apply (CPU
+        tensors, non-f32 logits, rows past the register row engines, no product left)."""
+        mask, i, tc, assign = td["action_mask"], td["i"], td["to_choose"], td["assignment"]
+        dev = logits.device
+        if dev.type != "cuda" or any(x.device != dev for x in (mask, i, tc, assign)):
+            return None
+        if logits.dtype != torch.float32 or logits.dim() != 2 or logits.stride(-1) != 1:
+            return None
+        b, l = mask.shape
+        if (logits.shape != (b, l) or l > 2048 or assign.dtype != torch.int32 or tc.dim() != 2
+                or tc.shape[-1] == 0 or tc.dtype != torch.float32):
+            return None
+        p = td["freq"].shape[-2]
+        m, i, assign = mask.contiguous(), i.contiguous(), assign.contiguous()
+        ain = action_in.long().contiguous() if action_in is not None else None
+        s = nat.stream_of(m)
+        # the decoding strategy keeps every action and log-probability: never pooled
+        act = torch.empty(b, dtype=torch.int64, device=dev)
+        logp = torch.empty(b, dtype=torch.float32, device=dev)
+        assign_out = self._out(assign.shape, assign.dtype, dev, s)
+        mask_out = self._out(m.shape, m.dtype, dev, s)
+        i_out = self._out(i.shape, i.dtype, dev, s)
+        done = self._out((b, 1), torch.bool, dev, s)
+        reward = self._out((b, 1), torch.bool, dev, s)
+        nat.call("co_slap_decode_step", b, l, p, nat.ptr(logits), logits.stride(0), nat.ptr(m),
+                 float(tanh_clipping), float(temperature), mode, nat.ptr(ain), nat.ptr(act),
+                 nat.ptr(logp), seed, offset, nat.ptr(tc), tc.stride(0), nat.ptr(assign),
+                 nat.ptr(assign_out), nat.ptr(mask_out), nat.ptr(i), nat.ptr(i_out),
+                 nat.ptr(done), nat.ptr(reward), None, nat.ptr(status), s)
+        lb = self._known_lb(td["i"])
+        if lb is not None:
+            self._remember_lb(i_out, lb - 1)
+        sel = action_in if action_in is not None else act
+        set_many(td, {key: sel, "assignment": assign_out, "to_choose": tc[..., 1:],
+                      "action_mask": mask_out, "i": i_out, "reward": reward, "done": done})
+        return sel, logp
 
     def _get_reward(self, td, actions=None, check: bool = False) -> torch.Tensor:
         """``slap/env.py:131-143``: sum over orders of the closed pick tour (``actions``

@@ -190,7 +190,10 @@ class TSPFusedEpisode(_GraphEpisode):
         self.rows = policy == "teacher" and layout == "rows" and n <= 1024
         if policy == "teacher":
             assert actions is not None and actions.shape == (b, n)
-            self.acts = actions.long().contiguous() if self.rows else actions.t().contiguous()
+            # the episode owns its copy (the transposed layout always copied): a captured
+            # graph replays on these, whatever the caller later does to its tensor
+            self.acts = (actions.long().contiguous().clone() if self.rows
+                         else actions.t().contiguous())
         else:
             self.acts = torch.empty((n, b), dtype=torch.int64, device=d)
         self.mask = torch.empty((b, n), dtype=torch.bool, device=d)

@@ -9,8 +9,11 @@ Python reference (``sys.getrefcount``), no other C++ owner (``_use_count``: auto
 DLPack, TensorDict internals) and no view of its storage (storage use count) -- which is
 exactly when a fresh allocation would be indistinguishable from it.  Entries are keyed by
 (shape, dtype, device, stream): a reused buffer is written by a kernel queued on the same
-stream as every earlier reader, as the caching allocator's own reuse is.
+stream as every earlier reader, as the caching allocator's own reuse is.  At most
+``max_keys`` keys are kept (least recently used dropped first), so shape changes (a last
+partial batch, a validation batch size) do not accumulate device memory.
 """
+import collections
 import sys
 
 import torch
@@ -19,10 +22,11 @@ _storage_use_count = getattr(torch._C, "_storage_Use_Count", None)
 
 
 class OutputPool:
-    def __init__(self, per_key: int = 4, device_types=("cuda",)):
+    def __init__(self, per_key: int = 4, device_types=("cuda",), max_keys: int = 16):
         self.per_key = per_key
         self.device_types = device_types
-        self._slots = {}
+        self.max_keys = max_keys
+        self._slots = collections.OrderedDict()
 
     def empty(self, shape, dtype, device, stream=0):
         """A tensor of this shape/dtype on ``device`` that no one else can observe."""
@@ -31,7 +35,11 @@ class OutputPool:
         key = (tuple(shape), dtype, device, stream)
         slots = self._slots.get(key)
         if slots is None:
+            if len(self._slots) >= self.max_keys:
+                self._slots.popitem(last=False)  # the least recently used key
             slots = self._slots[key] = []
+        else:
+            self._slots.move_to_end(key)
         getrc, suc = sys.getrefcount, _storage_use_count
         for t in slots:
             # references while checking: the slot list, the loop variable, getrefcount's

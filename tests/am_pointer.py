@@ -98,3 +98,70 @@ def oracle_logits_fn(dec, dev):
         return dec.logits(first.to(dev), td["current_node"].to(dev), i.to(dev),
                           td["action_mask"].to(dev)).cpu()
     return fn
+
+
+class SLAPPointerDecoder(nn.Module):
+    """The fork's SLAP policy (``examples/slap.py:11-93``) in the AM decoder's shape
+    (``am/decoder.py:134-200``): node features ``cat(locs, dist_mat[:, 0, :])`` (the
+    Manhattan distance of every location to the depot) through ``Linear(3, H)``
+    (``SLAPInitEmbedding``), a zero step context (``SLAPContext``), a static dynamic
+    embedding (``StaticEmbedding``), so the query is the projected graph context
+    ``project_fixed_context(mean(h))`` alone; glimpse + pointer over ``action_mask``.
+    Random init, eval mode, on the device; key / value / logit projections precomputed
+    (``_precompute_cache``).  Rows e of a multistart batch use instance e % B."""
+
+    def __init__(self, locs_bl2, dev):
+        super().__init__()
+        g = torch.Generator().manual_seed(9)
+
+        def lin(i, o, bias=False):
+            m = nn.Linear(i, o, bias=bias)
+            with torch.no_grad():
+                m.weight.copy_(torch.randn(o, i, generator=g) / math.sqrt(i))
+                if bias:
+                    m.bias.copy_(0.1 * torch.randn(o, generator=g))
+            return m
+
+        self.init_embed = lin(3, H, bias=True)
+        self.wfix, self.wk, self.wv, self.wo, self.wl = (lin(H, H), lin(H, H), lin(H, H),
+                                                         lin(H, H), lin(H, H))
+        self.to(dev).eval()
+        locs = locs_bl2.to(dev)
+        with torch.no_grad():
+            dist0 = (locs[:, :1, :] - locs).abs().sum(-1)  # dist_mat[:, 0, :] (Manhattan)
+            h = self.init_embed(torch.cat((locs, dist0[..., None]), -1))  # [B, L, H]
+            b, n = h.shape[0], h.shape[1]
+            self.q = self.wfix(h.mean(1))  # graph context + zero step context
+            self.kt = self.wk(h).view(b, n, HEADS, H // HEADS).permute(0, 2, 3, 1)
+            self.v = self.wv(h).view(b, n, HEADS, H // HEADS).transpose(1, 2)
+            self.lt = self.wl(h).transpose(1, 2).contiguous()
+        self.b = b
+
+    @torch.no_grad()
+    def logits(self, mask):
+        e, n = mask.shape
+        rows = torch.arange(e, device=mask.device) % self.b
+        q = self.q[rows].view(e, HEADS, 1, H // HEADS)
+        att = (q @ self.kt[rows]) / math.sqrt(H // HEADS)
+        att = att.masked_fill(~mask.view(e, 1, 1, n), float("-inf"))
+        glimpse = self.wo((att.softmax(-1) @ self.v[rows]).reshape(e, H))
+        return (glimpse.unsqueeze(1) @ self.lt[rows]).squeeze(1) / math.sqrt(H)
+
+    def forward(self, td, hidden=None, num_starts: int = 0):
+        return self.logits(td["action_mask"]), td["action_mask"]
+
+    def pre_decoder_hook(self, td, env, hidden=None, num_starts: int = 0):
+        return td, env, hidden
+
+
+def slap_oracle_logits_fn(dec, dev, rows_total=None):
+    """The SLAP decoder on `dev` from the ORACLE's mask.  ``rows_total``: evaluate the
+    oracle's rows as the first rows of a batch of that many (the rest all-feasible), so
+    every GEMM has the device run's shapes and the rows get the device run's bits."""
+    def fn(td):
+        m = td["action_mask"].to(dev)
+        if rows_total is not None and rows_total > m.shape[0]:
+            pad = torch.ones((rows_total - m.shape[0], m.shape[1]), dtype=torch.bool, device=dev)
+            return dec.logits(torch.cat((m, pad), 0))[: m.shape[0]].cpu()
+        return dec.logits(m).cpu()
+    return fn

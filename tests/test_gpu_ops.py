@@ -241,3 +241,24 @@ def test_distance_matrix(dev, shape):
     assert got.shape == want.shape
     assert torch.allclose(got, want, rtol=2e-7, atol=1e-7)
     assert (got.diagonal(dim1=-2, dim2=-1) == 0).all()
+
+
+def test_gather_out_of_range_outside_env_raises(dev, monkeypatch):
+    """An out-of-range gather_by_index outside any env / decode loop (model code): the
+    error is recorded in the device's deferred word and raised by check_errors() (one host
+    read), by the next env status read, or at once with CO_SYNC_CHECKS=1."""
+    import rl4co_slap_amd as ra
+    from rl4co_slap_amd import _native as nat
+    from rl4co_slap_amd.utils.ops import gather_by_index
+
+    src = torch.randn(4, 10, 3, device=dev)
+    bad = torch.tensor([[1, 2], [3, 10], [0, 0], [9, 9]], device=dev)
+    gather_by_index(src, bad)  # queued: no sync here
+    with pytest.raises(RuntimeError, match="index out of range"):
+        ra.check_errors()
+    ra.check_errors()  # reported once: the word was cleared
+    monkeypatch.setattr(nat, "SYNC_CHECKS", True)
+    with pytest.raises(RuntimeError, match="index out of range"):
+        gather_by_index(src, bad)
+    ok = gather_by_index(src, bad.clamp(max=9))
+    assert torch.equal(ok, src.gather(1, bad.clamp(max=9)[..., None].expand(4, 2, 3)))

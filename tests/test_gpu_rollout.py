@@ -350,3 +350,40 @@ def test_nearest_sqrt_tie_lowest_index(dev, n):
     ep.run_eager()
     torch.cuda.synchronize()
     _check(ep.final_state(), a, r, tdf)
+
+
+@pytest.mark.parametrize("n", [97, 100, 112, 113])
+@pytest.mark.parametrize("layout", ["pomo_lb3", "strided", "pomo_lb3_strided", "contiguous"])
+def test_tsp_reward_row_kernel_layouts(dev, n, layout):
+    """co_tsp_reward on row-major [B, N] actions through every row-kernel path: LDS-DMA
+    (contiguous, instance batch a multiple of the wave's rows), 16-byte action pairs
+    (16-byte aligned rows with an even stride: strided slices, POMO instance batches not a
+    multiple of 4 -- TSP-100 takes 7 steps per lane there, an odd count: scalar loads) and
+    scalar loads.  Reward = -tour length of locs[e % LB] (the multistart row map) within
+    1e-5; invalid rows flagged."""
+    from oracle.ops import gather_by_index, get_tour_length
+    from rl4co_slap_amd import _native as nat
+
+    g = torch.Generator().manual_seed(n)
+    lb = 3 if layout.startswith("pomo") else 24
+    b = lb * (5 if layout.startswith("pomo") else 1)
+    locs = torch.rand(lb, n, 2, generator=g)
+    acts = torch.stack([torch.randperm(n, generator=g) for _ in range(b)])
+    acts[1, 4] = acts[1, 5]  # one invalid tour
+    width = n + 2 if layout.endswith("strided") else n
+    full = torch.zeros(b, width, dtype=torch.int64)
+    full[:, :n] = acts
+    a_dev = full.to(dev)[:, :n]
+    assert a_dev.stride(0) == width
+    reward = torch.empty(b, dtype=torch.float32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    l_dev = locs.to(dev)
+    nat.call("co_tsp_reward", b, n, n, nat.ptr(l_dev), lb, nat.ptr(a_dev), a_dev.stride(0),
+             a_dev.stride(1), 1, nat.ptr(reward), nat.ptr(status), nat.stream_of(l_dev))
+    rows = torch.arange(b) % lb
+    ref = -get_tour_length(gather_by_index(locs[rows], acts))
+    r = reward.cpu()
+    ok = torch.ones(b, dtype=torch.bool)
+    ok[1] = False
+    assert ((r[ok] - ref[ok]).abs() <= 1e-5 * ref[ok].abs().clamp(min=1)).all()
+    assert int(status.item()) & nat.ST_INVALID_TOUR

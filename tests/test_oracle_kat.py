@@ -178,3 +178,33 @@ def test_uniform_fill_oracle_grid_and_demand():
     k = np.rint(d * 40.0).astype(int)
     assert set(np.unique(k)) == set(range(1, 10))
     assert np.array_equal(uniform_fill(10, 0, 1, seed=5, offset=1), uniform_fill(14, 0, 1, seed=5)[4:])
+
+
+def test_slap_dropin_episode_hand_known_answer():
+    """The decode loop (constructive/base.py:229-251) on a hand-built SLAP instance with a
+    known greedy sequence and reward -- values worked out by hand from slap/env.py:38-143
+    and decoding.py:327-381, not produced by the oracle: 3 products, 4 locations on a line
+    x = 0, 1, 2, 3 (location 0 the depot, masked at reset); the policy's logits favour
+    location 3, then 1, then 2 (argmax over the still-free ones); to_choose = 0, 1, 2, so
+    product p takes step p's location: assignment [3, 1, 2]; orders [[0, 1], [2, 2]]:
+    order 0 is the closed tour 3 -> 1 -> 3 (length 4), order 1 a product picked twice
+    (length 0): reward -4; done after exactly P = 3 steps, every location then masked."""
+    from oracle.rollout import constructive_forward
+
+    env = SLAPOracle(n_products=3, n_aisles=1, n_locs=4, seed=0)
+    td = TD({"locs": torch.tensor([[[0.0, 0.0], [1.0, 0.0], [2.0, 0.0], [3.0, 0.0]]]),
+             "freq": torch.ones(1, 3, 1), "assignment": torch.full((1, 3), -1, dtype=torch.int),
+             "picklist": torch.tensor([[[0, 1], [2, 2]]]),
+             "depot_loc_dist": torch.tensor([[0.0, 1.0, 2.0, 3.0]])}, [1])
+    td = env.reset(td)
+    assert td["action_mask"].tolist() == [[False, True, True, True]]
+    table = torch.tensor([[0.0, 2.0, 1.0, 3.0]])
+    steps = []
+    out = constructive_forward(td, env, lambda t: steps.append(1) or table, decode_type="greedy")
+    assert out["actions"].tolist() == [[3, 1, 2]]
+    assert len(steps) == 3
+    fin = out["td"]
+    assert fin["assignment"].tolist() == [[3, 1, 2]]
+    assert fin["action_mask"].tolist() == [[False, False, False, False]]
+    assert bool(fin["done"].all()) and fin["i"].tolist() == [[3]]
+    assert float(out["reward"][0]) == -4.0

@@ -57,7 +57,14 @@ else:
     np.random.seed(1234)
     b = 65536 if args.kernel.endswith("b65536") else 16384
     td = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
-    if args.kernel.startswith("slap_fused_random"):
+    if args.kernel.startswith("slap_stepwise"):  # slap_stepwise_{closest,teacher}[_b65536]
+        pol = "closest" if "closest" in args.kernel else "teacher"
+        acts = None
+        if pol == "teacher":
+            torch.manual_seed(4321)
+            acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
+        ep = engine.SLAPStepwiseEpisode(td, acts, policy=pol)
+    elif args.kernel.startswith("slap_fused_random"):
         torch.manual_seed(4321)
         acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
         ep = engine.SLAPFusedEpisode(td, acts, policy="teacher")
