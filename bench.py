@@ -271,8 +271,18 @@ def step_kernels_vs_copy(dev):
 
 
 def cpu_threads():
-    # the box's CPU share (OMP_NUM_THREADS is set to it on the GPU pool), not the whole host
+    """Threads for the CPU baseline: the CPU share this process was given.  On the GPU pool
+    a one-GPU job owns 16 of the host's CPUs (OMP_NUM_THREADS is set to that share);
+    os.cpu_count() counts the whole host, whose other CPUs belong to the jobs on its other
+    GPUs -- running 256 threads there would time oversubscription, not the reference."""
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+
+
+def _spread(times, work):
+    """min / median / max rate over the timed episodes (the first, a warm-up, dropped)."""
+    ts = sorted(times[1:])
+    return {"value": work / ts[len(ts) // 2], "value_min": work / ts[-1], "value_max": work / ts[0],
+            "episodes": len(ts)}
 
 
 def host_cpu():
@@ -299,7 +309,7 @@ def host_cpu():
             "aten_capability": torch.backends.cpu.get_cpu_capability()}
 
 
-def cpu_baseline_tsp(locs, acts, episodes=3):
+def cpu_baseline_tsp(locs, acts, episodes=5):
     """The oracle (reference op sequence on CPU torch) on the same TSP workload."""
     from oracle.envs import TSPOracle
     from oracle.rollout import rollout
@@ -316,15 +326,14 @@ def cpu_baseline_tsp(locs, acts, episodes=3):
         t0 = time.perf_counter()
         rollout(env, td, lambda td: acts[:, next(it)])
         times.append(time.perf_counter() - t0)
-    med = sorted(times[1:])[len(times[1:]) // 2]
-    return {"value": b * n / med, "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {**_spread(times, b * n), "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle (CPU PyTorch restatement) TSP-{n} teacher-forced rollout: reset + "
                       f"{n} x _step + get_reward with the double validity sort, B={b} (the full "
-                      f"GPU workload), median of {episodes} episodes after 1 warm-up, "
-                      f"torch.set_num_threads({threads})"}
+                      f"GPU workload), median (min / max beside it) of {episodes} episodes after "
+                      f"1 warm-up, torch.set_num_threads({threads}) = the job's CPU share"}
 
 
-def cpu_baseline_slap(b=16384, episodes=2):
+def cpu_baseline_slap(b=16384, episodes=5):
     """The oracle's SLAP rollout at config 4's batch (the GPU modes' B=16,384): the
     closest-free policy, the per-batch Python loop of slap/env.py:61-62 and the per-order
     reward loop kept.  The instances' grid columns (identical for every instance: the
@@ -354,15 +363,16 @@ def cpu_baseline_slap(b=16384, episodes=2):
         t0 = time.perf_counter()
         rollout(env, td, slap_closest_free_action)
         times.append(time.perf_counter() - t0)
-    med = sorted(times[1:])[len(times[1:]) // 2]
-    return {"value": b * 20 / med, "unit": "env-steps/s", "cores": cpu_threads(),
+    return {**_spread(times, b * 20), "unit": "env-steps/s", "cores": cpu_threads(),
+            "kind": "port",
             "sample": f"oracle SLAP rollout (closest-free policy, per-batch Python loop of "
-                      f"slap/env.py:61-62 kept), B={b}, median of {episodes}"}
+                      f"slap/env.py:61-62 kept), B={b}, median (min / max) of {episodes} "
+                      f"episodes after 1 warm-up"}
 
 
-def cpu_baseline_cvrp(b=16384, n=100, episodes=2):
-    """The oracle's CVRP-100 rollout with the nearest-feasible policy (config 3 recipe,
-    smaller B), including get_reward's Python capacity loop."""
+def cpu_baseline_cvrp(b=32768, n=100, episodes=5):
+    """The oracle's CVRP-100 rollout with the nearest-feasible policy (config 3 recipe and
+    batch), including get_reward's Python capacity loop."""
     from oracle.envs import CVRPOracle, cvrp_nearest_action
     from oracle.rollout import rollout
     from oracle.td import TD
@@ -382,11 +392,11 @@ def cpu_baseline_cvrp(b=16384, n=100, episodes=2):
         _, _, acts = rollout(env, td, cvrp_nearest_action)
         times.append(time.perf_counter() - t0)
         steps = acts.shape[1]
-    med = sorted(times[1:])[len(times[1:]) // 2]
-    return {"value": b * steps / med, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle CVRP-{n} rollout, nearest-feasible policy, B={b}, T={steps} "
-                      f"steps, get_reward with the validity + capacity loop, median of "
-                      f"{episodes}"}
+    return {**_spread(times, b * steps), "unit": "env-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle CVRP-{n} rollout, nearest-feasible policy, B={b} (config 3, the "
+                      f"GPU batch), T={steps} steps, get_reward with the validity + capacity "
+                      f"loop, median (min / max) of {episodes} episodes after 1 warm-up"}
 
 
 def pmc_traffic(target, kernel_prefix):
@@ -452,7 +462,11 @@ def main():
         "data": "synthetic: seeded torch.rand TSP instances, teacher-forced argsort actions",
         "config": {"workload": f"TSP-{n} B={b}/GPU teacher-forced episode (reset + {n} env steps + "
                                "reward + validity) as one fused launch (co_tsp_rollout_ex on the "
-                               "reference's row-major [B, N] actions)",
+                               "reference's row-major [B, N] actions; BASELINE config 2). A "
+                               "final-state-only episode: the per-step TensorDict states are not "
+                               "written to HBM, so its env-steps/s is not comparable with a "
+                               "per-step loop -- that figure is `tsp_stepwise`",
+                   "episode_kind": "fused, final state only",
                    "batch_per_gpu": b, "num_loc": n, "env_steps_per_episode": n,
                    "parallelism": f"dp{world}: disjoint instance shards, no data-path collective"},
         "roofline": {"bound": "hbm",
@@ -469,18 +483,51 @@ def main():
     }
     out["config"]["input_batches_cycled"] = n_rot
 
+    # ---- the contract-faithful per-step TSP loop: one launch per env step,
+    # every step's TensorDict state written to and re-read from HBM (2N+50 B per env-step,
+    # + the episode reward's 16N+4 B amortised), HIP graph of reset + N steps + reward
+    k = max(3, args.steps // 5)
+    sw = TSPStepwiseEpisode(locs, acts, policy="teacher", check=True).capture()
+    wall_s, ev_s = timed(sw.replay, k, 2, world, dev)
+    assert int(sw.status.item()) == 0, "TSP stepwise episode status"
+    del sw
+    t_s = max_over_ranks(wall_s, world, dev)
+    sw_bytes = 2 * n + 50 + (16 * n + 4) / n
+    out["tsp_stepwise"] = {
+        "value": world * b * n * k / t_s, "unit": "env-steps/s", "ms_per_episode": t_s / k * 1e3,
+        "workload": f"TSP-{n} B={b}/GPU teacher-forced episode, one co_tsp_step launch per env "
+                    "step (state in HBM between steps, as the reference loop), reset + reward "
+                    "included, HIP graph",
+        "launches_per_step": 1, "alg_bytes_per_env_step": sw_bytes,
+        "achieved_GBps": b * n * sw_bytes * k / ev_s / 1e9,
+        "frac": b * n * sw_bytes * k / ev_s / 1e9 / HBM_PEAK_GBS,
+        "frac_wall": b * n * sw_bytes * k / wall_s / 1e9 / HBM_PEAK_GBS}
+    # ---- SLAP at the north star's batch (B = 65,536; examples/slap.py instance)
+    slap65 = bench_slap(65536, k, world, rank, dev)
+    fc, sc = slap65["slap_fused_closest"], slap65["slap_stepwise_graph"]
+    s_traffic, s_src = pmc_traffic("slap_fused_closest_b65536", "slap_group_kernel<16, 8, true>")
+    out["slap_b65536"] = {
+        "value": fc["value"], "unit": "env-steps/s", "ms_per_episode": fc["ms_per_episode"],
+        "workload": "SLAP (examples/slap.py:75-76: L=100, P=20 products, O=20 orders x K=5) "
+                    "B=65,536/GPU, closest-free policy: reset + 20 env steps + pick-tour reward "
+                    "as one fused launch (co_slap_rollout); final state only, like the TSP "
+                    "headline",
+        "roofline": {"bound": "hbm", "kernel": "slap_group_kernel<16,8,true> (co_slap_rollout)",
+                     "achieved": fc["achieved_GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": fc["achieved_GBps"] / HBM_PEAK_GBS, "traffic": s_traffic,
+                     "traffic_source": s_src, "bytes_per_launch": 65536 * 2754,
+                     "launch_us": fc["launch_us"]},
+        "stepwise": {"value": sc["value"], "ms_per_episode": sc["ms_per_episode"],
+                     "launches_per_step": 1, "policy": sc["policy"],
+                     "alg_bytes_per_env_step": 234 + 1684 / 20,
+                     "frac_wall": sc["value"] / world * (234 + 1684 / 20) / 1e9 / HBM_PEAK_GBS}}
+
     if not args.no_modes:
         modes = {}
-        # stepwise: one launch per env step, TensorDict state in HBM (2N+50 B/step)
-        sw = TSPStepwiseEpisode(locs, acts, policy="teacher", check=True).capture()
-        k = max(3, args.steps // 5)
-        wall_s, ev_s = timed(sw.replay, k, 2, world, dev)
-        t_s = max_over_ranks(wall_s, world, dev)
         modes["tsp_stepwise_graph"] = {
-            "value": world * b * n * k / t_s, "ms_per_episode": t_s / k * 1e3,
+            "value": out["tsp_stepwise"]["value"], "ms_per_episode": t_s / k * 1e3,
             "bytes_per_env_step": 2 * n + 50,
             "achieved_GBps_incl_reset_reward": b * n * (2 * n + 50) * k / ev_s / 1e9}
-        del sw
         # in-kernel nearest-unvisited policy, fused
         ne = TSPFusedEpisode(locs, None, policy="nearest", check=True)
         sn = lambda: ne._launch(sh)  # noqa: E731
@@ -498,9 +545,8 @@ def main():
         modes["dropin_slap_b65536"] = bench_dropin_slap(65536, k, world, rank, dev)
         # SLAP (examples/slap.py instance), closest-free policy: fused and stepwise
         modes.update(bench_slap(args.slap_batch, k, world, rank, dev))
-        # the north star's "SLAP at batch 65,536": fused and stepwise
-        modes.update({k2 + "_b65536": v for k2, v in
-                      bench_slap(65536, k, world, rank, dev).items()})
+        # the north star's "SLAP at batch 65,536": fused and stepwise (measured above)
+        modes.update({k2 + "_b65536": v for k2, v in slap65.items()})
         # POMO TSP-100 (config 5): 1,024 instances x 100 starts per GPU, decode-fused steps
         # on HBM-resident logits, shared baseline + RCCL all-gather of per-instance results
         # default decode math = certified (exact greedy actions, logp within 1e-5)
@@ -529,9 +575,61 @@ def main():
             out["cpu_baseline_cvrp"] = cpu_baseline_cvrp()
     if rank == 0:
         out["build"] = _native.provenance()  # the sources the measured library came from
-        print(json.dumps(out), flush=True)
+        out["summary"] = summarize(out)
+        # contract keys first, then the short summary, the long mode tables last
+        order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                 "roofline", "cpu_baseline", "summary", "tsp_stepwise", "slap_b65536"]
+        final = {key: out[key] for key in order if key in out}
+        final.update({key: v for key, v in out.items() if key not in final})
+        print(json.dumps(final), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def summarize(out):
+    """The figures a reader needs first, in one short record: every per-GPU rate with its
+    HBM fraction, the drop-in loops' launches / GPU / host time per step."""
+    r = lambda x, d=3: None if x is None else round(float(x), d)  # noqa: E731
+    sm = {"tsp100_fused_final_state": {"env_steps_s": r(out["value"], 0),
+                                       "frac": r(out["roofline"]["frac"]),
+                                       "frac_wall": r(out["roofline"]["frac_wall"])}}
+    if "tsp_stepwise" in out:
+        t = out["tsp_stepwise"]
+        sm["tsp100_stepwise"] = {"env_steps_s": r(t["value"], 0), "frac": r(t["frac"]),
+                                 "frac_wall": r(t["frac_wall"])}
+    if "slap_b65536" in out:
+        t = out["slap_b65536"]
+        sm["slap_b65536_fused"] = {"env_steps_s": r(t["value"], 0),
+                                   "frac": r(t["roofline"]["frac"])}
+        sm["slap_b65536_stepwise"] = {"env_steps_s": r(t["stepwise"]["value"], 0),
+                                      "frac_wall": r(t["stepwise"]["frac_wall"])}
+    modes = out.get("modes", {})
+    for name in ("dropin_tsp100", "dropin_cvrp100", "dropin_slap_b16384", "dropin_slap_b65536"):
+        m = modes.get(name)
+        if not m:
+            continue
+        steps = m.get("episode_steps") or m.get("env_steps_per_episode") or 100
+        sm[name] = {"env_steps_s": r(m["value"], 0), "ms_per_episode": r(m["ms_per_episode"]),
+                    "launches_per_step": m.get("launches_per_step"),
+                    "gpu_us_per_step": r(m["gpu_ms_per_episode"] * 1e3 / steps, 2),
+                    "host_us_per_step_b64": r(m.get("host_us_per_loop_step_b64",
+                                                    m.get("host_us_per_step_b64")), 2),
+                    "hbm_frac": r(m.get("hbm_frac"))}
+    for name in ("pomo_tsp100", "cvrp_fused_nearest", "cvrp_stepwise_graph"):
+        m = modes.get(name)
+        if m:
+            sm[name] = {"env_steps_s": r(m["value"], 0), "ms_per_episode": r(m["ms_per_episode"]),
+                        "hbm_frac": r(m.get("hbm_frac"))}
+    sk = out.get("step_kernels_vs_copy", {})
+    if sk:
+        sm["step_kernels_frac_of_copy"] = {k2: r(v["frac_of_copy"]) for k2, v in sk.items()}
+    for name in ("cpu_baseline", "cpu_baseline_slap", "cpu_baseline_cvrp"):
+        c = out.get(name)
+        if c:
+            sm[name] = {"value": r(c["value"], 0), "min": r(c.get("value_min"), 0),
+                        "max": r(c.get("value_max"), 0), "threads": c["cores"]}
+    return sm
 
 
 def dry_run(args, world, rank, dev):

@@ -556,10 +556,13 @@ struct GreedyRow {
       const float ez = clip * 1.5e-6f + ldexpf(3.f, ec - 24);
       delta += 2.f * ((OPT & kOptTemp) ? ez / temp : ez);
     }
-    bool ok = __builtin_isfinite(L);
+    // the lane's runner-up: the largest v[k] other than sel's (masked and past-the-row slots
+    // are -inf; a NaN anywhere makes L NaN, which fails the finiteness test).  One max chain
+    // instead of a per-slot test (r04: certified kernel 20.3 -> 18.4 us at 102,400 x 100)
+    float r = -__builtin_inff();
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) ok &= (c0 + k >= N) | (c0 + k == sel) | (v[k] < -delta);
-    return ok;
+    for (int k = 0; k < EPL; ++k) r = fmaxf(r, c0 + k == sel ? -__builtin_inff() : v[k]);
+    return __builtin_isfinite(L) && r < -delta;
   }
 
   // greedy action of the row (valid on every lane of the group) and its logp
@@ -576,7 +579,11 @@ struct GreedyRow {
 // One row's greedy step on the GreedyRow engine: softmax_shift + select, or, with
 // kOptCert, the fast math certified per row and the exact math for any wave that holds an
 // uncertified valid row (wave-uniform branch: the group reductions need every lane).
-// Returns the action; L and lp as select().
+// Returns the action; L and lp as select().  The fallback recomputes into g itself (the
+// caller may read g.v afterwards: the full log-probabilities).  Measured and dropped (r04):
+// the fallback as a called (noinline) function -- the callee's registers count toward the
+// kernel's, 72 VGPRs; a waves-per-EU floor of 8 -- spills, 22.6-24.4 us; the compacted
+// tanh in the fallback -- 79 VGPRs.
 template <int OPT, int RL, int EPL, int VW>
 __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid, int N, float clip,
                                           float temp, int sl, int c0, float* lds_row, float& L,
@@ -785,8 +792,8 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     const uint8_t* mrow = mask_in + r * (int64_t)N;
     g.load(valid, N, lrow, mrow, c0);
     float lp, L;
-    const int sel = greedy_row<OPT>(g, valid, N, clip, temp, sl, c0, group_scratch<RL, EPL>(lds, grp),
-                                    L, lp, lrow, mrow);
+    const int sel = greedy_row<OPT>(g, valid, N, clip, temp, sl, c0,
+                                           group_scratch<RL, EPL>(lds, grp), L, lp, lrow, mrow);
     const bool feas0 = g.allowed(0);
     uint32_t left = 0u;
 #pragma unroll

@@ -104,8 +104,8 @@ __global__ __launch_bounds__(256) void slap_decode_greedy_kernel(
     const uint8_t* mrow = mask_in + r * (int64_t)L;
     g.load(valid, L, lrow, mrow, c0);
     float lp, lse;
-    const int sel = greedy_row<OPT>(g, valid, L, clip, temp, sl, c0, group_scratch<RL, EPL>(lds, grp),
-                                    lse, lp, lrow, mrow);
+    const int sel = greedy_row<OPT>(g, valid, L, clip, temp, sl, c0,
+                                           group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
     const bool feas0 = g.allowed(0);
 #pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {  // the selected location leaves the mask
@@ -339,7 +339,7 @@ __global__ __launch_bounds__(256) void cvrp_decode_greedy_kernel(
     g.load(valid, NC, lrow, mrow, c0);
     float lp, lse;
     const int sel = greedy_row<OPT>(g, valid, NC, clip, temp, sl, c0,
-                                    group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
+                                           group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
     const bool feas0 = g.allowed(0);
     cr.template apply<RL>(e, valid, r, sl, grp, c0, sel, status);
     if (valid && sl == 0) {

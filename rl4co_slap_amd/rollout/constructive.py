@@ -138,7 +138,7 @@ class ConstructivePolicy(nn.Module):
                 lb = step + k  # cannot be all done before then: no host sync until
             logits, mask = decode(td, hidden, num_starts)
             act = actions[..., step] if actions is not None else None
-            # decode + env step as one launch where the env provides it (TSP), else both
+            # decode + env step as one launch where the env provides it (TSP, CVRP, SLAP)
             nxt = strategy.step_env_fused(logits, mask, td, env, action=act)
             if nxt is None:
                 td = strategy.step(logits, mask, td, action=act)

@@ -263,7 +263,8 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
 
     def step_env_fused(self, logits, mask, td, env, action=None):
         """``self.step`` followed by ``env.step`` as ONE launch, when the env offers it
-        (``TSPEnv.decode_and_step``: ``co_tsp_decode_step``) and nothing in between could
+        (``decode_and_step``: ``co_tsp_decode_step`` / ``co_slap_decode_step`` /
+        ``co_cvrp_decode_step``) and nothing in between could
         observe the difference: the env's own ``step``, the mask the env holds, no full
         log-probabilities / top-k / top-p.  Same outputs, same RNG use; returns the next
         td, or None when the fused path does not apply (the caller runs both steps)."""

@@ -233,6 +233,15 @@ def test_fused_decode_env_step_equals_two_launches(dev, monkeypatch, name, decod
             kw = {"actions": acts}
         else:
             kw = {"decode_type": decode_type}
+            if name == "slap" and decode_type.startswith("multistart"):
+                # the reference's SLAP start nodes are s % 0xFFFFFFFF + 1 (ops.py:158-163):
+                # with all L = 100 starts the last one is location 100, out of range -- the
+                # reference's mask write raises (slap/env.py:61-62), here the status bit does
+                if no_fused:
+                    with pytest.raises(IndexError):
+                        pol(env.reset(TensorDict({k: v.clone().to(dev) for k, v in gen.items()},
+                                                 [b])), env, phase="test", decode_math=math, **kw)
+                kw["num_starts"] = 50
         out = pol(td, env, phase="test", return_actions=True, decode_math=math, **kw)
         outs.append((out, {k: td[k].clone() for k in keys}))
         launches.append(len(calls))

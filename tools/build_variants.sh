@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 mkdir -p tools/_variants
 ONLY=""
 if [ "$1" = "-s" ]; then ONLY=$2; shift 2; fi
-ALL="tsp cvrp slap ops decode_step decode_tsp rollout nearest"
+ALL="tsp cvrp slap ops decode_step decode_tsp decode_env rollout nearest"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Iinclude"
 while [ $# -ge 2 ]; do
   if [ -n "$ONLY" ]; then
@@ -26,7 +26,7 @@ while [ $# -ge 2 ]; do
     ) &
   else
     /opt/rocm/bin/hipcc $FLAGS -shared $2 -o tools/_variants/libco_env_$1.so \
-      rl4co_slap_amd/csrc/{tsp,cvrp,slap,ops,decode_step,decode_tsp,rollout,nearest}.hip &
+      rl4co_slap_amd/csrc/{tsp,cvrp,slap,ops,decode_step,decode_tsp,decode_env,rollout,nearest}.hip &
   fi
   shift 2
 done

@@ -15,6 +15,32 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 
+def decode_kernel_us(b, n, dev, flag, reps=100):
+    """co_tsp_decode_step (greedy, tanh clip 10) at B x N on a half-visited state, HIP events."""
+    from rl4co_slap_amd import _native
+
+    g = torch.Generator().manual_seed(3)
+    logits = torch.randn(b, n, generator=g).to(dev)
+    mask = (torch.rand(b, n, generator=g) < 0.5).to(dev)
+    mask[:, 0] = True
+    i = torch.full((b, 1), n // 2, dtype=torch.int64, device=dev)
+    first = torch.zeros(b, dtype=torch.int64, device=dev)
+    outs = [torch.empty(b, dtype=torch.int64, device=dev), torch.empty(b, device=dev),
+            torch.empty((b, n), dtype=torch.bool, device=dev),
+            torch.empty((b, 1), dtype=torch.int64, device=dev),
+            torch.empty(b, dtype=torch.int64, device=dev),
+            torch.empty(b, dtype=torch.bool, device=dev), torch.empty(b, dtype=torch.bool, device=dev)]
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    launch = _native.bind("co_tsp_decode_step", b, n, logits.data_ptr(), n, mask.data_ptr(),
+                          10.0, 1.0, flag, None, outs[0].data_ptr(), outs[1].data_ptr(), 0, 0,
+                          outs[2].data_ptr(), i.data_ptr(), outs[3].data_ptr(), first.data_ptr(),
+                          outs[4].data_ptr(), 0, outs[5].data_ptr(), outs[6].data_ptr(), None,
+                          st.data_ptr())
+    _, ev = bench.timed(lambda: launch(sh), reps, 5, 1, dev)
+    return ev / reps * 1e6
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("mode")
@@ -59,6 +85,11 @@ def main():
         cyc = itertools.cycle([e._bound for e in eps])
         wall, ev = bench.timed(lambda: next(cyc)(sh), a.k, 2, 1, dev)
         out = {"launch_us": ev / a.k * 1e6, "wall_us": wall / a.k * 1e6, "batches": n_rot}
+    elif a.mode == "decode_kernels":  # the fused TSP decode step alone, POMO shape, clip 10
+        out = {}
+        for name, flag in (("certified", _native.DECODE_CERTIFIED), ("fast", _native.DECODE_FAST),
+                           ("exact", 0)):
+            out[name] = round(decode_kernel_us(102400, 100, dev, flag), 3)
     elif a.mode == "gen":
         out = bench.bench_generate_uniform(65536, 100, dev)
     else:
