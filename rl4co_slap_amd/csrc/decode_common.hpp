@@ -615,9 +615,12 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+  // one row group per wave: the grid covers B (no grid-stride loop, so no values are
+  // hoisted into registers across row groups -- r04: certified 71 -> fewer VGPRs)
+  const int64_t base = wid * RPW;
+  if (base >= B) return;  // wave-uniform
+  do {
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
@@ -637,7 +640,7 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
       action_out[r] = sel;
       if (logp_sel) logp_sel[r] = lp;
     }
-  }
+  } while (0);
 }
 
 template <int RL, int EPL, bool VEC, int OPT>
@@ -651,9 +654,12 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+  // one row group per wave: the grid covers B (no grid-stride loop, so no values are
+  // hoisted into registers across row groups -- r04: certified 71 -> fewer VGPRs)
+  const int64_t base = wid * RPW;
+  if (base >= B) return;  // wave-uniform
+  do {
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
@@ -674,7 +680,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
       action_out[r] = mode == CO_DECODE_EVALUATE ? a_in : (int64_t)d.sel;
       if (logp_sel) logp_sel[r] = d.lp;
     }
-  }
+  } while (0);
 }
 
 // Decode step fused with TSPEnv._step: the row's logits and action_mask are read once;
@@ -694,12 +700,15 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
   // UNR rows per lane group per iteration: every load of all UNR rows (logits, mask,
   // i, first_node, action, ll accumulator) is issued before any row's math
-  for (int64_t base = wid * RPW * UNR; base < B; base += nwaves * RPW * UNR) {
+  // one row group per wave: the grid covers B (no grid-stride loop, so no values are
+  // hoisted into registers across row groups -- r04: certified 71 -> fewer VGPRs)
+  const int64_t base = wid * RPW * UNR;
+  if (base >= B) return;  // wave-uniform
+  do {
     DecodeRow<RL, EPL, VEC, OPT> d[UNR];
     int64_t rr[UNR], ain[UNR], iv[UNR], fv[UNR];
     bool vv[UNR];
@@ -756,7 +765,7 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
         step_reward[r] = 0;
       }
     }
-  }
+  } while (0);
 }
 
 // Greedy decode step fused with TSPEnv._step on the GreedyRow engine (the POMO /
@@ -773,10 +782,13 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+  // one row group per wave: the grid covers B (no grid-stride loop, so no values are
+  // hoisted into registers across row groups -- r04: certified 71 -> fewer VGPRs)
+  const int64_t base = wid * RPW;
+  if (base >= B) return;  // wave-uniform
+  do {
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
@@ -814,7 +826,7 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
       done[r] = !any_left;
       step_reward[r] = 0;
     }
-  }
+  } while (0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1070,7 +1082,7 @@ inline unsigned decode_grid(int64_t B, int N, int unr = 1) {
   const int rl = N <= 16 ? CO_RL16 : N <= 32 ? CO_RL32 : N <= 64 ? CO_RL64
                : N <= 128 ? CO_RL128 : N <= 256 ? CO_RL256 : 64;
   const int64_t waves = ((B + unr - 1) / unr * rl + 63) / 64;
-  return grid_for(waves, 4, 256 * 32);
+  return grid_for(waves, 4, (int64_t)1 << 30);  // every row group gets its wave
 }
 
 // widest GreedyRow load (4 / 2 / 1 elements) the row length, stride and pointers allow

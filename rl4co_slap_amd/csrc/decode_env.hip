@@ -21,6 +21,31 @@
 
 namespace {
 
+// ------------------------------------------------------------------ env staging
+// The env data a row's transition needs is fetched into the wave's LDS by LDS-DMA
+// (global_load_lds_dword: each lane one dword from its own address, no VGPR destination)
+// before the row's logits are loaded, so it is in flight with them and holds no register
+// through the decode -- the decode's registers (and the certified kernels' exact fallback)
+// set the kernel's VGPR count, as in co_tsp_decode_step.  The decode's wait for its logits
+// (vmcnt counts in issue order) also covers the DMA; the transition reads the stage after
+// an explicit drain + wave barrier.
+template <class F>
+__device__ __forceinline__ void dma_dwords(int n, uint32_t* lds_dst, F src) {
+  const int lane = lane_id();
+  for (int base = 0; base < n; base += 64) {  // wave-uniform trip count
+    const int k = base + lane;
+    if (k < n)
+      __builtin_amdgcn_global_load_lds((const void*)src(k), (lds_void*)(lds_dst + base), 4, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void stage_ready() {
+  __builtin_amdgcn_s_waitcnt(0);  // every DMA (and any pending load) landed
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ------------------------------------------------------------------ SLAP transition
 struct SlapEpi {
   int P;
@@ -33,46 +58,50 @@ struct SlapEpi {
   int64_t* i_out;
   uint8_t* done;
   uint8_t* reward;
+  float* ll_accum;
 };
 
-// The row's SLAP scalars and (out of place) the assignment row, loaded with the logits.
-template <int RL>
-struct SlapRow {
-  static constexpr int AU = 2;  // assignment entries per lane held in registers (P <= 2*RL)
-  int64_t it = 0;
-  float prod = 0.f;
-  int32_t av[AU];
+// Per wave (RPW rows): [i_in: 2 RPW dwords][product: RPW][ll: RPW][assignment: RPW * P]
+__host__ __device__ inline int slap_stage_dwords(int rpw, int P) { return rpw * (4 + P); }
 
-  __device__ __forceinline__ void load(const SlapEpi& e, bool valid, int64_t r, int sl) {
-    if (valid) prod = e.to_choose[r * e.tc_stride];  // one address per group: a broadcast
-    if (valid && sl == 0) it = e.i_in[r];
-#pragma unroll
-    for (int u = 0; u < AU; ++u) {
-      const int c = sl + RL * u;
-      av[u] = (valid && e.assign_in != e.assign_out && c < e.P) ? e.assign_in[r * e.P + c] : 0;
-    }
+template <int RL>
+struct SlapStage {
+  static constexpr int RPW = 64 / RL;
+  uint32_t* s;  // the wave's stage
+  int P;
+  __device__ __forceinline__ void issue(const SlapEpi& e, int64_t base, int nr) const {
+    const int Pn = P;
+    dma_dwords(2 * nr, s, [&](int k) { return reinterpret_cast<const uint32_t*>(e.i_in + base) + k; });
+    dma_dwords(nr, s + 2 * RPW, [&](int k) { return e.to_choose + (base + k) * e.tc_stride; });
+    if (e.ll_accum) dma_dwords(nr, s + 3 * RPW, [&](int k) { return e.ll_accum + base + k; });
+    if (e.assign_in != e.assign_out)
+      dma_dwords(nr * Pn, s + 4 * RPW, [&](int k) { return e.assign_in + base * Pn + k; });
+  }
+  __device__ __forceinline__ int64_t i_of(int g) const {
+    return (int64_t)(((uint64_t)s[2 * g + 1] << 32) | s[2 * g]);
+  }
+  __device__ __forceinline__ float prod_of(int g) const { return __uint_as_float(s[2 * RPW + g]); }
+  __device__ __forceinline__ float ll_of(int g) const { return __uint_as_float(s[3 * RPW + g]); }
+  __device__ __forceinline__ int32_t asg_of(int g, int c) const {
+    return (int32_t)s[4 * RPW + g * P + c];
   }
 
-  // slap/env.py:50-62 for action a_raw (python indexing already applied to the mask by
-  // the caller); `sl == 0` writes the row scalars.  Returns false when the product index
-  // is out of range (the reference's advanced-index write raises).
-  __device__ __forceinline__ bool store(const SlapEpi& e, int64_t r, int sl, int64_t a_raw) const {
-    int64_t p = (int64_t)(int)prod;  // .to(torch.int), slap/env.py:52
+  // slap/env.py:50-62 for action a_raw of row r (group g); `sl == 0` writes the row
+  // scalars.  Returns false when the product index is out of range (the reference's
+  // advanced-index write raises).
+  __device__ __forceinline__ bool store(const SlapEpi& e, int64_t r, int g, int sl,
+                                        int64_t a_raw) const {
+    int64_t p = (int64_t)(int)prod_of(g);  // .to(torch.int), slap/env.py:52
     if (p < 0) p += e.P;
     const bool p_ok = p >= 0 && p < e.P;
     const int32_t av_new = (int32_t)a_raw;  // .to(torch.int), slap/env.py:53-54
     if (e.assign_in != e.assign_out) {      // the clone with [p] = action
-#pragma unroll
-      for (int u = 0; u < AU; ++u) {
-        const int c = sl + RL * u;
-        if (c < e.P) e.assign_out[r * e.P + c] = c == p ? av_new : av[u];
-      }
-      for (int c = sl + RL * AU; c < e.P; c += RL)
-        e.assign_out[r * e.P + c] = c == p ? av_new : e.assign_in[r * e.P + c];
+      for (int c = sl; c < e.P; c += RL) e.assign_out[r * e.P + c] = c == p ? av_new : asg_of(g, c);
     } else if (sl == 0 && p_ok) {
       e.assign_out[r * e.P + p] = av_new;
     }
     if (sl == 0) {
+      const int64_t it = i_of(g);
       e.done[r] = it == (int64_t)(e.P - 1);  // slap/env.py:57
       e.i_out[r] = it + 1;
       e.reward[r] = 0;
@@ -86,41 +115,47 @@ template <int RL, int EPL, int VW, int OPT>
 __global__ __launch_bounds__(256) void slap_decode_greedy_kernel(
     int64_t B, int L, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int64_t* __restrict__ action_out,
-    float* __restrict__ logp_sel, float* __restrict__ ll_accum, int32_t* status, SlapEpi e) {
+    float* __restrict__ logp_sel, int32_t* status, SlapEpi e) {
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const SlapStage<RL> st{s_stage + (threadIdx.x >> 6) * slap_stage_dwords(RPW, e.P), e.P};
+  // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
+  // registers across row groups)
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+  const int64_t base = wid * RPW;
+  if (base >= B) return;  // wave-uniform
+  {
+    const int nr = (int)(B - base < RPW ? B - base : RPW);
+    st.issue(e, base, nr);
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
-    SlapRow<RL> sr;
-    sr.load(e, valid, r, sl);
-    const float acc = (valid && sl == 0 && ll_accum) ? ll_accum[r] : 0.f;
     GreedyRow<RL, EPL, VW> g;
     const float* lrow = logits + r * lstride;
     const uint8_t* mrow = mask_in + r * (int64_t)L;
     g.load(valid, L, lrow, mrow, c0);
     float lp, lse;
     const int sel = greedy_row<OPT>(g, valid, L, clip, temp, sl, c0,
-                                           group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
+                                    group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
     const bool feas0 = g.allowed(0);
 #pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {  // the selected location leaves the mask
       const int off = sel - (c0 + 4 * j);
       if ((unsigned)off < 4u) g.mw[j] &= ~(0xffu << (8 * off));
     }
-    if (!valid) continue;  // no group operation below
-    g.store_mask(L, e.mask_out + r * (int64_t)L, c0);
-    const bool p_ok = sr.store(e, r, sl, sel);
-    if (sl == 0) {
-      if (lse != lse && !feas0) set_status(status, CO_ST_INFEASIBLE);
-      if (!p_ok) set_status(status, CO_ST_INDEX_RANGE);
-      action_out[r] = sel;
-      if (logp_sel) logp_sel[r] = lp;
-      if (ll_accum) ll_accum[r] = acc + lp;
+    stage_ready();
+    if (valid) {
+      g.store_mask(L, e.mask_out + r * (int64_t)L, c0);
+      const bool p_ok = st.store(e, r, grp, sl, sel);
+      if (sl == 0) {
+        if (lse != lse && !feas0) set_status(status, CO_ST_INFEASIBLE);
+        if (!p_ok) set_status(status, CO_ST_INDEX_RANGE);
+        action_out[r] = sel;
+        if (logp_sel) logp_sel[r] = lp;
+        if (e.ll_accum) e.ll_accum[r] = st.ll_of(grp) + lp;
+      }
     }
   }
 }
@@ -131,21 +166,24 @@ __global__ __launch_bounds__(256) void slap_decode_step_kernel(
     int64_t B, int L, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int mode,
     const int64_t* __restrict__ action_in, int64_t* __restrict__ action_out,
-    float* __restrict__ logp_sel, uint64_t seed, uint64_t offset, float* __restrict__ ll_accum,
-    int32_t* status, SlapEpi e) {
+    float* __restrict__ logp_sel, uint64_t seed, uint64_t offset, int32_t* status, SlapEpi e) {
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const SlapStage<RL> st{s_stage + (threadIdx.x >> 6) * slap_stage_dwords(RPW, e.P), e.P};
+  // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
+  // registers across row groups)
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+  const int64_t base = wid * RPW;
+  if (base >= B) return;  // wave-uniform
+  {
+    const int nr = (int)(B - base < RPW ? B - base : RPW);
+    st.issue(e, base, nr);
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
     const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
-    SlapRow<RL> sr;
-    sr.load(e, valid, r, sl);
-    const float acc = (valid && sl == 0 && ll_accum) ? ll_accum[r] : 0.f;
     DecodeRow<RL, EPL, VEC, OPT> d;
     d.run(valid, L, logits + r * lstride, mask_in + r * (int64_t)L, clip, temp, mode, a_in, seed,
           offset, row, sl, grp, group_scratch<RL, EPL>(lds, grp));
@@ -155,29 +193,31 @@ __global__ __launch_bounds__(256) void slap_decode_step_kernel(
 #pragma unroll
     for (int k = 0; k < EPL; ++k)
       if (a_ok && c0 + k == a) d.mk[k] = 0;
-    if (!valid) continue;
-    uint8_t* orow = e.mask_out + r * (int64_t)L;
-    if (VEC) {
+    stage_ready();
+    if (valid) {
+      uint8_t* orow = e.mask_out + r * (int64_t)L;
+      if (VEC) {
 #pragma unroll
-      for (int j = 0; j < EPL / 4; ++j)
-        if (c0 + 4 * j < L)
-          *reinterpret_cast<uint32_t*>(orow + c0 + 4 * j) =
-              (uint32_t)d.mk[4 * j] | ((uint32_t)d.mk[4 * j + 1] << 8) |
-              ((uint32_t)d.mk[4 * j + 2] << 16) | ((uint32_t)d.mk[4 * j + 3] << 24);
-    } else {
+        for (int j = 0; j < EPL / 4; ++j)
+          if (c0 + 4 * j < L)
+            *reinterpret_cast<uint32_t*>(orow + c0 + 4 * j) =
+                (uint32_t)d.mk[4 * j] | ((uint32_t)d.mk[4 * j + 1] << 8) |
+                ((uint32_t)d.mk[4 * j + 2] << 16) | ((uint32_t)d.mk[4 * j + 3] << 24);
+      } else {
 #pragma unroll
-      for (int k = 0; k < EPL; ++k)
-        if (c0 + k < L) orow[c0 + k] = d.mk[k];
-    }
-    const bool p_ok = sr.store(e, r, sl, a_raw);
-    if (sl == 0) {
-      if (mode == CO_DECODE_EVALUATE && (a_in < 0 || a_in >= L))
-        set_status(status, CO_ST_INDEX_RANGE);  // the logp gather (decoding.py:365)
-      if (mode != CO_DECODE_EVALUATE && !d.feas) set_status(status, CO_ST_INFEASIBLE);
-      if (!a_ok || !p_ok) set_status(status, CO_ST_INDEX_RANGE);
-      action_out[r] = a_raw;
-      if (logp_sel) logp_sel[r] = d.lp;
-      if (ll_accum) ll_accum[r] = acc + d.lp;
+        for (int k = 0; k < EPL; ++k)
+          if (c0 + k < L) orow[c0 + k] = d.mk[k];
+      }
+      const bool p_ok = st.store(e, r, grp, sl, a_raw);
+      if (sl == 0) {
+        if (mode == CO_DECODE_EVALUATE && (a_in < 0 || a_in >= L))
+          set_status(status, CO_ST_INDEX_RANGE);  // the logp gather (decoding.py:365)
+        if (mode != CO_DECODE_EVALUATE && !d.feas) set_status(status, CO_ST_INFEASIBLE);
+        if (!a_ok || !p_ok) set_status(status, CO_ST_INDEX_RANGE);
+        action_out[r] = a_raw;
+        if (logp_sel) logp_sel[r] = d.lp;
+        if (e.ll_accum) e.ll_accum[r] = st.ll_of(grp) + d.lp;
+      }
     }
   }
 }
@@ -195,72 +235,58 @@ struct CvrpEpi {
   uint8_t* done;
   uint8_t* reward;
   uint8_t* mask_out;
+  float* ll_accum;
 };
 
-// The lane's EPL columns of a CVRP row: visited bytes as 4-column words, the demand of
-// each column (column c: demand[c - 1]; the depot column's slot unused), the row
-// scalars.  Loads are Chunk<3> accesses (byte-aligned dwords, dword-aligned dwordx4):
-// the [B, N+1] byte rows and the [B, N] demand rows are aligned to neither.
-template <int EPL>
-struct CvrpRow {
-  uint32_t vw[EPL / 4];
-  float dm[EPL];
-  float used = 0.f, cap = 0.f;
+// Per wave (RPW rows): [demand: RPW*N][visited bytes: RPW*(N+1) rounded up to dwords]
+// [used: RPW][capacity: RPW][ll: RPW].  The visited rows of a wave are one contiguous,
+// 4-byte-aligned byte range (the launcher requires RPW*(N+1) % 4 == 0 and an aligned
+// buffer), fetched as whole dwords; the last partial wave's trailing bytes (< 4) by bytes.
+__host__ __device__ inline int cvrp_vis_dwords(int rpw, int N) { return (rpw * (N + 1) + 3) / 4; }
+__host__ __device__ inline int cvrp_stage_dwords(int rpw, int N) {
+  return rpw * N + cvrp_vis_dwords(rpw, N) + 3 * rpw;
+}
 
-  __device__ __forceinline__ void load(const CvrpEpi& e, bool valid, int64_t r, int c0) {
-    using F = typename Chunk<3>::F;
-    using M = typename Chunk<3>::M;
-    const int NC = e.N + 1;
-    const uint8_t* vrow = e.vis_in + r * (int64_t)NC;
-    const float* drow = e.demand + r * (int64_t)e.N;
-    if (valid) {  // every lane: the row's scalars (one address per group: a broadcast)
-      used = e.used_in[r];
-      cap = e.vcap[r];
+template <int RL, int EPL>
+struct CvrpStage {
+  static constexpr int RPW = 64 / RL;
+  uint32_t* s;
+  int N;
+  __device__ __forceinline__ uint32_t* dem() const { return s; }
+  __device__ __forceinline__ uint32_t* vis() const { return s + RPW * N; }
+  __device__ __forceinline__ uint32_t* sc() const { return s + RPW * N + cvrp_vis_dwords(RPW, N); }
+
+  __device__ __forceinline__ void issue(const CvrpEpi& e, int64_t base, int nr) const {
+    const int Nn = N, NC = N + 1;
+    dma_dwords(nr * Nn, dem(), [&](int k) { return e.demand + base * Nn + k; });
+    const uint8_t* vrow = e.vis_in + base * NC;
+    const int nvb = nr * NC, nvw = nvb >> 2;
+    dma_dwords(nvw, vis(), [&](int k) { return reinterpret_cast<const uint32_t*>(vrow) + k; });
+    if (nvb & 3) {  // the buffer's last bytes (the last partial wave only): plain loads
+      const int lane = lane_id();
+      uint8_t* vb = reinterpret_cast<uint8_t*>(vis() + nvw);
+      if (lane < (nvb & 3)) vb[lane] = vrow[4 * nvw + lane];
     }
-#pragma unroll
-    for (int j = 0; j < EPL / 4; ++j) {
-      const int c = c0 + 4 * j;
-      uint32_t v = 0u;
-      float d[4] = {0.f, 0.f, 0.f, 0.f};
-      if (valid && c >= 4 && c + 4 <= NC) {  // interior chunk: demand[c-1 .. c+2]
-        v = (uint32_t) * reinterpret_cast<const M*>(vrow + c);
-        const F x = *reinterpret_cast<const F*>(drow + (c - 1));
-        d[0] = x[0];
-        d[1] = x[1];
-        d[2] = x[2];
-        d[3] = x[3];
-      } else if (valid && c < NC) {  // the depot's chunk / the row's partial last chunk
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (c + q < NC) {
-            v |= (uint32_t)vrow[c + q] << (8 * q);
-            if (c + q >= 1) d[q] = drow[c + q - 1];
-          }
-      }
-      vw[j] = v;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dm[4 * j + q] = d[q];
-    }
+    dma_dwords(nr, sc(), [&](int k) { return e.used_in + base + k; });
+    dma_dwords(nr, sc() + RPW, [&](int k) { return e.vcap + base + k; });
+    if (e.ll_accum) dma_dwords(nr, sc() + 2 * RPW, [&](int k) { return e.ll_accum + base + k; });
   }
 
-  // cvrp/env.py:73-105 + get_action_mask (:137-149) for action a_raw, the same
-  // arithmetic as co_cvrp_step.  Group-wide (every lane of the wave active); returns
-  // done and writes the visited / mask rows and (sl == 0) the row scalars.
-  template <int RL>
-  __device__ __forceinline__ void apply(const CvrpEpi& e, bool valid, int64_t r, int sl, int grp,
-                                        int c0, int64_t a_raw, int32_t* status) {
-    const int N = e.N, NC = N + 1;
-    const bool bad = a_raw < 0 || a_raw > N;
-    // selected demand demand[clamp(a - 1, 0, N - 1)] (column csel) from its owner lane
-    const int csel = (int)(a_raw - 1 < 0 ? 0 : (a_raw - 1 > N - 1 ? N - 1 : a_raw - 1)) + 1;
-    const int owner = grp * RL + csel / EPL, slot = csel % EPL;
-    float mine = 0.f;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) mine = k == slot ? dm[k] : mine;
-    const float dsel = __shfl(mine, owner, 64);
-    const float u = (used + dsel) * ((a_raw != 0) ? 1.0f : 0.0f);
+  // cvrp/env.py:73-105 + get_action_mask (:137-149) for action a_raw of row r (group g),
+  // the same arithmetic as co_cvrp_step, on the staged row.  Group-wide (every lane of the
+  // wave active); writes the visited / mask rows and (sl == 0) the row scalars.
+  __device__ __forceinline__ void apply(const CvrpEpi& e, bool valid, int64_t r, int g, int sl,
+                                        int c0, int64_t a_raw, int32_t* status) const {
+    const int Nn = N, NC = N + 1;
+    const float* dm_s = reinterpret_cast<const float*>(dem()) + g * Nn;
+    const uint8_t* vb_s = reinterpret_cast<const uint8_t*>(vis()) + g * NC;
+    const float used = __uint_as_float(sc()[g]), cap = __uint_as_float(sc()[RPW + g]);
+    const bool bad = a_raw < 0 || a_raw > Nn;
+    // the selected demand demand[clamp(a - 1, 0, N - 1)]
+    const int dsi = (int)(a_raw - 1 < 0 ? 0 : (a_raw - 1 > Nn - 1 ? Nn - 1 : a_raw - 1));
+    const float u = (used + dm_s[dsi]) * ((a_raw != 0) ? 1.0f : 0.0f);
     const int a = bad ? -1 : (int)a_raw;
-    uint32_t mk[EPL / 4];
+    uint32_t vw[EPL / 4], mk[EPL / 4];
     uint32_t cnt = 0u;
     bool feas = false;
 #pragma unroll
@@ -269,14 +295,20 @@ struct CvrpRow {
       const int nown = valid ? (NC - c < 0 ? 0 : (NC - c > 4 ? 4 : NC - c)) : 0;
       const uint32_t own = nown >= 4 ? 0xffffffffu : (1u << (8 * nown)) - 1u;
       const uint32_t cust = c == 0 ? own & ~0xffu : own;  // the depot column excluded
-      uint32_t x = vw[j];
+      uint32_t x = 0u;
+      float d[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool in = q < nown;
+        x |= in ? (uint32_t)vb_s[c + q] << (8 * q) : 0u;
+        d[q] = (in && c + q >= 1) ? dm_s[c + q - 1] : 0.f;
+      }
       const int ea = a - c;  // the action's byte, if in this chunk: scatter(..., 1)
       if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
       vw[j] = x;
-      const uint32_t over = ((dm[4 * j] + u > cap) ? 0x80u : 0u) |
-                            ((dm[4 * j + 1] + u > cap) ? 0x8000u : 0u) |
-                            ((dm[4 * j + 2] + u > cap) ? 0x800000u : 0u) |
-                            ((dm[4 * j + 3] + u > cap) ? 0x80000000u : 0u);
+      const uint32_t over = ((d[0] + u > cap) ? 0x80u : 0u) | ((d[1] + u > cap) ? 0x8000u : 0u) |
+                            ((d[2] + u > cap) ? 0x800000u : 0u) |
+                            ((d[3] + u > cap) ? 0x80000000u : 0u);
       const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
       const uint32_t m = ((~(nz | over) & 0x80808080u) >> 7) & cust;
       cnt = __builtin_amdgcn_sad_u8(x & own, 0u, cnt);
@@ -285,7 +317,7 @@ struct CvrpRow {
     }
     cnt = grp_reduce<RL>(cnt, [](uint32_t x, uint32_t y) { return x + y; });
     const uint64_t gm = RL == 64 ? ~0ull : ((1ull << RL) - 1ull);
-    const bool anyf = ((__ballot(feas) >> (RL * grp)) & gm) != 0ull;
+    const bool anyf = ((__ballot(feas) >> (RL * g)) & gm) != 0ull;
     if (!valid) return;
     if (sl == 0) mk[0] |= (uint32_t) !((a_raw == 0) && anyf);  // cvrp/env.py:146-148
     using M = typename Chunk<3>::M;
@@ -314,39 +346,45 @@ struct CvrpRow {
       e.reward[r] = 0;
     }
   }
+  __device__ __forceinline__ float ll_of(int g) const { return __uint_as_float(sc()[2 * RPW + g]); }
 };
 
 template <int RL, int EPL, int VW, int OPT>
 __global__ __launch_bounds__(256) void cvrp_decode_greedy_kernel(
     int64_t B, int NC, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int64_t* __restrict__ action_out,
-    float* __restrict__ logp_sel, float* __restrict__ ll_accum, int32_t* status, CvrpEpi e) {
+    float* __restrict__ logp_sel, int32_t* status, CvrpEpi e) {
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const CvrpStage<RL, EPL> st{s_stage + (threadIdx.x >> 6) * cvrp_stage_dwords(RPW, e.N), e.N};
+  // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
+  // registers across row groups)
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+  const int64_t base = wid * RPW;
+  if (base >= B) return;  // wave-uniform
+  {
+    const int nr = (int)(B - base < RPW ? B - base : RPW);
+    st.issue(e, base, nr);
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
-    CvrpRow<EPL> cr;
-    cr.load(e, valid, r, c0);
-    const float acc = (valid && sl == 0 && ll_accum) ? ll_accum[r] : 0.f;
     GreedyRow<RL, EPL, VW> g;
     const float* lrow = logits + r * lstride;
     const uint8_t* mrow = mask_in + r * (int64_t)NC;
     g.load(valid, NC, lrow, mrow, c0);
     float lp, lse;
     const int sel = greedy_row<OPT>(g, valid, NC, clip, temp, sl, c0,
-                                           group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
+                                    group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
     const bool feas0 = g.allowed(0);
-    cr.template apply<RL>(e, valid, r, sl, grp, c0, sel, status);
+    stage_ready();
+    st.apply(e, valid, r, grp, sl, c0, sel, status);
     if (valid && sl == 0) {
       if (lse != lse && !feas0) set_status(status, CO_ST_INFEASIBLE);
       action_out[r] = sel;
       if (logp_sel) logp_sel[r] = lp;
-      if (ll_accum) ll_accum[r] = acc + lp;
+      if (e.ll_accum) e.ll_accum[r] = st.ll_of(grp) + lp;
     }
   }
 }
@@ -356,38 +394,56 @@ __global__ __launch_bounds__(256) void cvrp_decode_step_kernel(
     int64_t B, int NC, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int mode,
     const int64_t* __restrict__ action_in, int64_t* __restrict__ action_out,
-    float* __restrict__ logp_sel, uint64_t seed, uint64_t offset, float* __restrict__ ll_accum,
-    int32_t* status, CvrpEpi e) {
+    float* __restrict__ logp_sel, uint64_t seed, uint64_t offset, int32_t* status, CvrpEpi e) {
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const CvrpStage<RL, EPL> st{s_stage + (threadIdx.x >> 6) * cvrp_stage_dwords(RPW, e.N), e.N};
+  // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
+  // registers across row groups)
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * RPW; base < B; base += nwaves * RPW) {
+  const int64_t base = wid * RPW;
+  if (base >= B) return;  // wave-uniform
+  {
+    const int nr = (int)(B - base < RPW ? B - base : RPW);
+    st.issue(e, base, nr);
     const int64_t row = base + grp;
     const bool valid = row < B;
     const int64_t r = valid ? row : 0;
     const int64_t a_in = (mode == CO_DECODE_EVALUATE && valid) ? action_in[r] : 0;
-    CvrpRow<EPL> cr;
-    cr.load(e, valid, r, c0);
-    const float acc = (valid && sl == 0 && ll_accum) ? ll_accum[r] : 0.f;
     DecodeRow<RL, EPL, VEC, OPT> d;
     d.run(valid, NC, logits + r * lstride, mask_in + r * (int64_t)NC, clip, temp, mode, a_in,
           seed, offset, row, sl, grp, group_scratch<RL, EPL>(lds, grp));
     const int64_t a_raw = mode == CO_DECODE_EVALUATE ? a_in : (int64_t)d.sel;
-    cr.template apply<RL>(e, valid, r, sl, grp, c0, a_raw, status);
+    stage_ready();
+    st.apply(e, valid, r, grp, sl, c0, a_raw, status);
     if (valid && sl == 0) {
       if (mode == CO_DECODE_EVALUATE && (a_in < 0 || a_in >= NC))
         set_status(status, CO_ST_INDEX_RANGE);
       if (mode != CO_DECODE_EVALUATE && !d.feas) set_status(status, CO_ST_INFEASIBLE);
       action_out[r] = a_raw;
       if (logp_sel) logp_sel[r] = d.lp;
-      if (ll_accum) ll_accum[r] = acc + d.lp;
+      if (e.ll_accum) e.ll_accum[r] = st.ll_of(grp) + d.lp;
     }
   }
 }
 
 }  // namespace
+
+// lanes per row of the register row engines (decode_common.hpp's buckets)
+inline int row_lanes(int64_t N) {
+  return N <= 16 ? CO_RL16 : N <= 32 ? CO_RL32 : N <= 64 ? CO_RL64 : N <= 128 ? CO_RL128
+       : N <= 256 ? CO_RL256 : 64;
+}
+inline int row_epl(int64_t N) {
+  const int rl = row_lanes(N);
+  const int b = N <= 16 ? 16 : N <= 32 ? 32 : N <= 64 ? 64 : N <= 128 ? 128 : N <= 256 ? 256
+              : N <= 512 ? 512 : N <= 1024 ? 1024 : 2048;
+  const int e = b / rl;
+  return e < 4 ? 4 : e;
+}
+inline bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
 
 extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float* logits,
                                    int64_t lstride, const uint8_t* mask_in, float clip, float temp,
@@ -399,6 +455,7 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
                                    uint8_t* done, uint8_t* step_reward, float* ll_accum,
                                    int32_t* status, void* stream) {
   if (B < 0 || L <= 0 || L > 64 * 32 || P <= 0 || P > (1 << 24)) return CO_E_INVAL;
+  const int mword = mode;
   const bool cert = (mode & CO_DECODE_CERTIFIED) != 0 && (mode & CO_DECODE_FAST) == 0;
   const bool fast = (mode & CO_DECODE_FAST) != 0;
   mode &= ~(CO_DECODE_FAST | CO_DECODE_CERTIFIED);
@@ -409,17 +466,31 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
       (mode == CO_DECODE_EVALUATE && !action_in))
     return CO_E_INVAL;
   if (mask_out == mask_in) return CO_E_INVAL;  // the mask is read by other lanes' decode
-  const SlapEpi epi{(int)P, to_choose, tc_stride, assign_in, assign_out, mask_out,
-                    i_in,   i_out,     done,      step_reward};
   const int64_t N = L;  // the row-dispatch macros' name for the row length
+  const int rpw = 64 / row_lanes(N);
+  const size_t shmem = (size_t)4 * slap_stage_dwords(rpw, (int)P) * 4;
+  const size_t lds_static = (size_t)4 * 64 * row_epl(N) * 4;
+  if (shmem + lds_static > 64 * 1024 || !aligned4(to_choose) || !aligned4(assign_in) ||
+      !aligned4(i_in) || (ll_accum && !aligned4(ll_accum))) {
+    // beyond the stage (huge P) or misaligned: the two launches it fuses
+    if (ll_accum) return CO_E_INVAL;
+    int rc = co_decode_step(B, L, logits, lstride, mask_in, clip, temp, mword, action_in,
+                            action_out, logp_sel, nullptr, seed, offset, status, stream);
+    if (rc != CO_OK) return rc;
+    return co_slap_step(B, L, P, mode == CO_DECODE_EVALUATE ? action_in : action_out, to_choose,
+                        tc_stride, assign_in, assign_out, mask_in, mask_out, i_in, i_out, done,
+                        step_reward, status, stream);
+  }
+  const SlapEpi epi{(int)P, to_choose, tc_stride, assign_in, assign_out, mask_out,
+                    i_in,   i_out,     done,      step_reward, ll_accum};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(decode_grid(B, (int)N)), block(256);
+  const dim3 grid((unsigned)((B + rpw * 4 - 1) / (rpw * 4))), block(256);
   if (mode == CO_DECODE_GREEDY) {
 #define CO_SDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \
                     (slap_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), grid, block, \
-                    0, s, B, (int)N, logits, lstride, mask_in, clip, temp, action_out,         \
-                    logp_sel, ll_accum, status, epi)
+                    shmem, s, B, (int)N, logits, lstride, mask_in, clip, temp, action_out,     \
+                    logp_sel, status, epi)
     switch (greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr)) {
       case 4: CO_ROW_DISPATCH(CO_SDG, 4); break;
       default: CO_ROW_DISPATCH(CO_SDG, 3);
@@ -429,8 +500,8 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
   }
 #define CO_SDS(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH(hipLaunchKernelGGL, (slap_decode_step_kernel<RL, EPL, V, OPT>), grid, block, \
-                  0, s, B, (int)N, logits, lstride, mask_in, clip, temp, mode, action_in,       \
-                  action_out, logp_sel, seed, offset, ll_accum, status, epi)
+                  shmem, s, B, (int)N, logits, lstride, mask_in, clip, temp, mode, action_in,   \
+                  action_out, logp_sel, seed, offset, status, epi)
   if (decode_vec_ok(logits, lstride, mask_in, N) &&
       (reinterpret_cast<uintptr_t>(mask_out) & 3) == 0) {
     CO_ROW_DISPATCH(CO_SDS, true);
@@ -452,6 +523,7 @@ extern "C" int co_cvrp_decode_step(int64_t B, int64_t Ncust, const float* logits
                                    uint8_t* mask_out, float* ll_accum, int32_t* status,
                                    void* stream) {
   if (B < 0 || Ncust <= 0 || Ncust + 1 > 64 * 32) return CO_E_INVAL;
+  const int mword = mode;
   const bool cert = (mode & CO_DECODE_CERTIFIED) != 0 && (mode & CO_DECODE_FAST) == 0;
   const bool fast = (mode & CO_DECODE_FAST) != 0;
   mode &= ~(CO_DECODE_FAST | CO_DECODE_CERTIFIED);
@@ -465,17 +537,32 @@ extern "C" int co_cvrp_decode_step(int64_t B, int64_t Ncust, const float* logits
   // visited / mask rows are fine within a row, but a lane group's stores must not reach
   // another group's unread row, so the outputs are separate buffers
   if (mask_out == mask_in || vis_out == vis_in) return CO_E_INVAL;
-  const CvrpEpi epi{(int)Ncust, demand,  used_in, used_out, vcap,       vis_in,
-                    vis_out,    cur_out, done,    step_reward, mask_out};
   const int64_t N = Ncust + 1;  // row length (depot + customers)
+  const int rpw = 64 / row_lanes(N);
+  const size_t shmem = (size_t)4 * cvrp_stage_dwords(rpw, (int)Ncust) * 4;
+  const size_t lds_static = (size_t)4 * 64 * row_epl(N) * 4;
+  if (shmem + lds_static > 64 * 1024 || (rpw * N) % 4 != 0 || !aligned4(vis_in) ||
+      !aligned4(demand) || !aligned4(used_in) || !aligned4(vcap) ||
+      (ll_accum && !aligned4(ll_accum))) {
+    // beyond the stage or misaligned rows: the two launches it fuses
+    if (ll_accum) return CO_E_INVAL;
+    int rc = co_decode_step(B, N, logits, lstride, mask_in, clip, temp, mword, action_in,
+                            action_out, logp_sel, nullptr, seed, offset, status, stream);
+    if (rc != CO_OK) return rc;
+    return co_cvrp_step(B, Ncust, mode == CO_DECODE_EVALUATE ? action_in : action_out, demand,
+                        used_in, used_out, vcap, vis_in, vis_out, cur_out, done, step_reward,
+                        mask_out, status, nullptr, stream);
+  }
+  const CvrpEpi epi{(int)Ncust, demand,  used_in, used_out,    vcap,     vis_in,
+                    vis_out,    cur_out, done,    step_reward, mask_out, ll_accum};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(decode_grid(B, (int)N)), block(256);
+  const dim3 grid((unsigned)((B + rpw * 4 - 1) / (rpw * 4))), block(256);
   if (mode == CO_DECODE_GREEDY) {
 #define CO_CDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \
                     (cvrp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), grid, block, \
-                    0, s, B, (int)N, logits, lstride, mask_in, clip, temp, action_out,         \
-                    logp_sel, ll_accum, status, epi)
+                    shmem, s, B, (int)N, logits, lstride, mask_in, clip, temp, action_out,     \
+                    logp_sel, status, epi)
     switch (greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr)) {
       case 4: CO_ROW_DISPATCH(CO_CDG, 4); break;
       default: CO_ROW_DISPATCH(CO_CDG, 3);
@@ -485,8 +572,8 @@ extern "C" int co_cvrp_decode_step(int64_t B, int64_t Ncust, const float* logits
   }
 #define CO_CDS(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH(hipLaunchKernelGGL, (cvrp_decode_step_kernel<RL, EPL, V, OPT>), grid, block, \
-                  0, s, B, (int)N, logits, lstride, mask_in, clip, temp, mode, action_in,       \
-                  action_out, logp_sel, seed, offset, ll_accum, status, epi)
+                  shmem, s, B, (int)N, logits, lstride, mask_in, clip, temp, mode, action_in,   \
+                  action_out, logp_sel, seed, offset, status, epi)
   if (decode_vec_ok(logits, lstride, mask_in, N)) {
     CO_ROW_DISPATCH(CO_CDS, true);
   } else {

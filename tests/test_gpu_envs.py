@@ -560,3 +560,51 @@ def test_slap_reward_paths_vs_oracle(dev, b, l, p, o, k):
     picks[0, 1, 2] = p + 3
     _, st = _slap_reward_direct(dev, locs, assign, picks)
     assert st & 8
+
+
+@pytest.mark.parametrize("n", [3, 16, 20, 24, 36, 100, 128, 252, 256, 260])
+@pytest.mark.parametrize("b", [1, 15, 16, 17, 33, 1000])
+def test_tsp_step_kernel_paths_vs_reference(dev, b, n):
+    """co_tsp_step on arbitrary (not policy-reachable) states through every kernel path
+    (the flat 16-byte-chunk kernel for N % 4 == 0, 16 <= N <= 256 incl. the partial last
+    wave's tail dwords; the lane-group and tile kernels otherwise): random mask bytes with
+    all-zero rows, actions at chunk / row boundaries, out-of-range actions (status bit, no
+    byte cleared), first_mode 0 / 1, in and out of place -- against tsp/env.py:67-93."""
+    from rl4co_slap_amd import _native as nat
+
+    g = torch.Generator().manual_seed(b * 1000 + n)
+    mask = torch.rand(b, n, generator=g) < 0.6
+    mask[:: 5] = False  # rows with nothing left
+    act = torch.randint(0, n, (b,), generator=g)
+    act[1::7] = n - 1
+    act[2::11] = 0
+    bad = torch.zeros(b, dtype=torch.bool)
+    if b > 3:
+        act[3] = n  # out of range
+        bad[3] = True
+    i = torch.randint(0, n, (b, 1), generator=g)
+    first = torch.randint(0, n, (b,), generator=g)
+    for first_mode in (0, 1):
+        for inplace in (False, True):
+            m_d = mask.to(dev)
+            m_o = m_d if inplace else torch.empty_like(m_d)
+            i_d, f_d = i.to(dev), first.to(dev)
+            i_o, f_o = torch.empty_like(i_d), torch.empty_like(f_d)
+            cur = torch.empty_like(f_d)
+            done = torch.empty(b, dtype=torch.bool, device=dev)
+            rw = torch.ones(b, dtype=torch.bool, device=dev)
+            st = torch.zeros(1, dtype=torch.int32, device=dev)
+            a_d = act.to(dev)
+            nat.call("co_tsp_step", b, n, nat.ptr(a_d), nat.ptr(m_d), nat.ptr(m_o), nat.ptr(i_d),
+                     nat.ptr(i_o), nat.ptr(f_d), nat.ptr(f_o), nat.ptr(cur), nat.ptr(done),
+                     nat.ptr(rw), first_mode, None, nat.ptr(st), nat.stream_of(m_d))
+            want = mask.clone()
+            ok = ~bad
+            want[ok.nonzero().squeeze(1), act[ok]] = False
+            assert torch.equal(m_o.cpu(), want), (first_mode, inplace)
+            assert torch.equal(done.cpu(), ~want.any(-1))
+            assert torch.equal(i_o.cpu(), i + 1)
+            assert torch.equal(f_o.cpu(), act if first_mode == 1 else first)
+            assert torch.equal(cur.cpu(), act)
+            assert not bool(rw.any())
+            assert bool(int(st.item()) & nat.ST_INDEX_RANGE) == bool(bad.any())
