@@ -926,8 +926,7 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
         env = CVRPEnv(generator_params=dict(num_loc=n), device=dev)
         pol = ConstructivePolicy(None, LogitsDecoder(lambda td: logits), env_name="cvrp")
         steps, calls = [], []
-        real = env.decode_and_step
-        env.decode_and_step = lambda *a, **kw: calls.append(1) or real(*a, **kw)
+        real = count_fused_calls(env, calls)
 
         def run():
             td = env.reset(TensorDict(dict(data), [bb]))
@@ -947,9 +946,21 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
                                 "(co_cvrp_decode_step per step)"})
         else:
             out["host_us_per_step_b64"] = t / kk / T * 1e6
-        env.decode_and_step = real
+        env.decode_and_step, env.native_decode_and_step = real
     out["host_below_kernels"] = out["host_us_per_step_b64"] < out["gpu_us_per_step"]
     return out
+
+
+def count_fused_calls(env, calls):
+    """Count the env's fused decode + step calls (the native step glue or the Python
+    decode_and_step); returns the originals to restore."""
+    real = (env.decode_and_step, env.native_decode_and_step)
+    env.decode_and_step = lambda *a, **kw: calls.append(1) or real[0](*a, **kw)
+    native = real[1]()
+    if native is not None:
+        counted = lambda *a, **kw: calls.append(1) or native(*a, **kw)  # noqa: E731
+        env.native_decode_and_step = lambda: counted
+    return real
 
 
 def bench_dropin_slap(b, k, world, rank, dev):
@@ -989,8 +1000,7 @@ def bench_dropin_slap(b, k, world, rank, dev):
                    else SLAPPointerDecoder(data["locs"], dev))
             pol = ConstructivePolicy(None, dec, env_name="slap", tanh_clipping=10.0)
             calls = []
-            real = env.decode_and_step
-            env.decode_and_step = lambda *a, **kw: calls.append(1) or real(*a, **kw)
+            real = count_fused_calls(env, calls)
 
             def run():
                 td = env.reset(TensorDict(dict(data.items()), [bb]))
@@ -1014,7 +1024,7 @@ def bench_dropin_slap(b, k, world, rank, dev):
                     out["am_decoder"] = m
             else:
                 out[key + "host_us_per_step_b64"] = t / kk / P * 1e6
-            env.decode_and_step = real
+            env.decode_and_step, env.native_decode_and_step = real
             del env, pol, dec, data
     out["decode_fused_kernel_us"] = slap_decode_step_kernel_us(b, dev)
     out["host_below_kernel"] = out["host_us_per_step_b64"] < out["decode_fused_kernel_us"]

@@ -309,6 +309,8 @@ class _TorchStep:
         self.tsp_step_td = bound(mod.tsp_step_td, "co_tsp_decode_step")
         self.decode_step = bound(mod.decode_step, "co_decode_step")
         self.cvrp_step = bound(mod.cvrp_step, "co_cvrp_step")
+        self.slap_step_td = bound(mod.slap_step_td, "co_slap_decode_step")
+        self.cvrp_step_td = bound(mod.cvrp_step_td, "co_cvrp_decode_step")
         self.clear_pool = mod.clear_pool
 
 

@@ -470,27 +470,53 @@ __global__ __launch_bounds__(64 * WAVES) void cvrp_step_rows_kernel(
       const uint32_t dep = !((a_raw == 0) && anyf);
       uint8_t* vdst = vis_out + byte0;
       uint8_t* mdst = mask + byte0;
+      // Stores as whole dwords: the dword a row shares with the previous row of its quad
+      // (its first, when the row does not start 4-aligned) is written by this row's lane 0
+      // with the previous row's bytes merged in (one lane shuffle of each word); the
+      // previous row skips it.  A quad of 4 rows starts and ends 4-aligned (4 (N+1) bytes
+      // from a 4-aligned start), so no dword is shared between waves -- only the buffer's
+      // last row, when B % 4 != 0, stores its trailing bytes one by one.
+      uint32_t mm[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int cb = 4 * (sl + G * j) - s;
+        mm[j] = cb <= 0 ? m[j] | (dep << (8 * -cb)) : m[j];
+      }
+      const int jl = (ndw - 1) / G;  // the slot of the row's last dword (group-uniform)
+      uint32_t lastv = 0u, lastm = 0u;
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j == jl) {
+          lastv = V[q][j];
+          lastm = mm[j];
+        }
+      const int sp = (int)((byte0 - NC) & 3);  // the previous row's first-byte offset
+      const int src = grp > 0 ? (grp - 1) * G + ((((sp + NC + 3) >> 2) - 1) % G) : lane;
+      const uint32_t prev_v = __shfl(lastv, src, 64), prev_m = __shfl(lastm, src, 64);
+      const bool tail_shared = ((byte0 + NC) & 3) != 0;  // the last dword holds row b + 1's bytes
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         const int k = sl + G * j;
         if (!valid || k >= ndw) continue;
-        const int cb = 4 * k - s;
-        uint32_t mk = m[j];
-        if (cb <= 0) mk |= dep << (8 * -cb);
-        const int lo = cb < 0 ? -cb : 0;
-        const int hi = NC - cb < 4 ? NC - cb : 4;
-        if (lo == 0 && hi == 4) {
-          reinterpret_cast<uint32_t*>(vdst - s)[k] = V[q][j];
-          reinterpret_cast<uint32_t*>(mdst - s)[k] = mk;
-        } else {  // the row's first / last dword: its own bytes only
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (e >= lo && e < hi) {
-              vdst[cb + e] = (uint8_t)(V[q][j] >> (8 * e));
-              mdst[cb + e] = (uint8_t)(mk >> (8 * e));
-            }
-          }
+        uint32_t vv = V[q][j], mv = mm[j];
+        if (k == 0 && s > 0) {  // shared with the previous row of the quad: merged
+          const uint32_t ownb = ~((1u << (8 * s)) - 1u);
+          vv = (vv & ownb) | (prev_v & ~ownb);
+          mv = (mv & ownb) | (prev_m & ~ownb);
         }
+        if (k == ndw - 1 && tail_shared) {
+          if (b + 1 < B) continue;  // the next row's lane 0 writes it
+          const int cb = 4 * k - s;  // the buffer's last row: its own bytes only
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (e < NC - cb) {
+              vdst[cb + e] = (uint8_t)(vv >> (8 * e));
+              mdst[cb + e] = (uint8_t)(mv >> (8 * e));
+            }
+          continue;
+        }
+        reinterpret_cast<uint32_t*>(vdst - s)[k] = vv;
+        reinterpret_cast<uint32_t*>(mdst - s)[k] = mv;
       }
       if (valid) {  // the row scalars, spread over the group's lanes
         if (sl == 0) used_out[b] = u;

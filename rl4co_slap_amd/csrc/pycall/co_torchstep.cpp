@@ -17,6 +17,7 @@
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 #include "co_env.h"
@@ -24,6 +25,8 @@
 namespace {
 
 using TspDecodeStep = decltype(&co_tsp_decode_step);
+using SlapDecodeStep = decltype(&co_slap_decode_step);
+using CvrpDecodeStep = decltype(&co_cvrp_decode_step);
 using DecodeStep = decltype(&co_decode_step);
 using CvrpStep = decltype(&co_cvrp_step);
 
@@ -356,6 +359,229 @@ PyObject* tsp_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
   return res;
 }
 
+// Wraps the 7 outputs, records i / lb, stores the new state in the td; shared tail of the
+// env step_td functions.  `extra` = (key, tensor) pairs to set besides the action key.
+PyObject* td_finish(PyObject* td, PyObject* key, PyObject* ain_o, at::Tensor& act,
+                    at::Tensor& logp, std::initializer_list<std::pair<const char*, at::Tensor*>> st,
+                    std::initializer_list<std::pair<const char*, PyObject*>> views,
+                    PyObject* lb_src, PyObject* lb_attr, const char* lb_dst) {
+  const long long lb = lb_src ? known(lb_src, lb_attr) : -1;
+  PyObject* a_o = THPVariable_Wrap(std::move(act));
+  PyObject* l_o = THPVariable_Wrap(std::move(logp));
+  if (!a_o || !l_o) {
+    Py_XDECREF(a_o);
+    Py_XDECREF(l_o);
+    return nullptr;
+  }
+  PyObject* sel = ain_o != Py_None ? ain_o : a_o;
+  int err = PyDict_SetItem(td, key, sel);
+  for (auto& kv : st) {
+    if (err) break;
+    PyObject* o = THPVariable_Wrap(std::move(*kv.second));
+    if (!o) {
+      err = -1;
+      break;
+    }
+    if (lb >= 0 && lb_dst && std::strcmp(kv.first, lb_dst) == 0)
+      err = remember(o, lb_attr, lb > 0 ? lb - 1 : 0);
+    if (!err) err = PyDict_SetItemString(td, kv.first, o);
+    Py_DECREF(o);
+  }
+  for (auto& kv : views) {
+    if (err) break;
+    err = PyDict_SetItemString(td, kv.first, kv.second);
+  }
+  PyObject* res = err ? nullptr : PyTuple_Pack(2, sel, l_o);
+  Py_DECREF(a_o);
+  Py_DECREF(l_o);
+  return res;
+}
+
+inline PyObject* td_tensor(PyObject* td, const char* k) {  // borrowed; nullptr if absent
+  PyObject* o = PyDict_GetItemString(td, k);
+  return (o && is_tensor(o)) ? o : nullptr;
+}
+
+// slap_step_td(fn, lb_attr, td, logits, mode, temp, clip, action_in, seed, offset, status,
+//              key) -> (action, logp) | None | error code
+// SLAPEnv.decode_and_step (envs/slap.py) on a dict-backed TensorDict in one call: reads
+// action_mask / i / to_choose / assignment / freq, launches co_slap_decode_step into fresh
+// outputs, stores assignment / to_choose[:, 1:] / action_mask / i / reward / done and the
+// action, records the done lower bound on the new i.
+PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 12) {
+    PyErr_SetString(PyExc_TypeError, "slap_step_td: 12 arguments");
+    return nullptr;
+  }
+  PyObject* lb_attr = a[1];
+  PyObject* td = a[2];
+  PyObject* key = a[11];
+  PyObject* ain_o = a[7];
+  if (!PyDict_Check(td) || !is_tensor(a[3]) || !is_tensor(a[10]) ||
+      (ain_o != Py_None && !is_tensor(ain_o)) || !PyUnicode_Check(key) || !PyUnicode_Check(lb_attr))
+    Py_RETURN_NONE;
+  PyObject *mask_o = td_tensor(td, "action_mask"), *i_o = td_tensor(td, "i"),
+           *tc_o = td_tensor(td, "to_choose"), *as_o = td_tensor(td, "assignment"),
+           *fr_o = td_tensor(td, "freq");
+  if (!mask_o || !i_o || !tc_o || !as_o || !fr_o) Py_RETURN_NONE;
+  const auto fn = fn_at<SlapDecodeStep>(a[0]);
+  const long mode = PyLong_AsLong(a[4]);
+  const double temp = PyFloat_AsDouble(a[5]), clip = PyFloat_AsDouble(a[6]);
+  const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[8]);
+  const uint64_t offset = PyLong_AsUnsignedLongLongMask(a[9]);
+  if (PyErr_Occurred()) return nullptr;
+  try {
+    const at::Tensor& logits = THPVariable_Unpack(a[3]);
+    const at::Tensor& mask = THPVariable_Unpack(mask_o);
+    const at::Tensor& i = THPVariable_Unpack(i_o);
+    const at::Tensor& tc = THPVariable_Unpack(tc_o);
+    const at::Tensor& asg = THPVariable_Unpack(as_o);
+    const at::Tensor& status = THPVariable_Unpack(a[10]);
+    const at::Tensor* ain = ain_o != Py_None ? &THPVariable_Unpack(ain_o) : nullptr;
+    const c10::Device dev = mask.device();
+    // the conditions envs/slap.py:decode_and_step checks
+    if (!dev.is_cuda() || logits.device() != dev || logits.scalar_type() != at::kFloat ||
+        logits.dim() != 2 || logits.stride(1) != 1 || mask.dim() != 2 ||
+        mask.scalar_type() != at::kBool || !mask.is_contiguous() || tc.dim() != 2 ||
+        tc.device() != dev || tc.scalar_type() != at::kFloat || tc.stride(1) != 1 ||
+        tc.size(1) < 1 || status.device() != dev || status.scalar_type() != at::kInt)
+      Py_RETURN_NONE;
+    const at::Tensor& fr = THPVariable_Unpack(fr_o);
+    const int64_t b = mask.size(0), l = mask.size(1);
+    if (fr.dim() < 2) Py_RETURN_NONE;
+    const int64_t p = fr.size(fr.dim() - 2);
+    if (logits.size(0) != b || logits.size(1) != l || l > 2048 || tc.size(0) != b ||
+        !fits(i, dev, at::kLong, b) || !fits(asg, dev, at::kInt, b * p) || asg.dim() != 2)
+      Py_RETURN_NONE;
+    if (ain && !fits(*ain, dev, at::kLong, b)) Py_RETURN_NONE;
+    const int64_t kb = up(8 * b);
+    const int64_t ko = g_slab.take(dev, 2 * kb);
+    at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
+    at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b});
+    Carver c;
+    const int64_t oa = c.take(4 * b * p), om = c.take(b * l), oi = c.take(8 * b), od = c.take(b),
+                  orw = c.take(b);
+    void* stream = current_stream(dev);
+    const c10::Storage st = g_state.acquire(dev, c.off, stream);
+    at::Tensor asg_out = view_of(st, at::kInt, oa, asg.sizes());
+    at::Tensor mask_out = view_of(st, at::kBool, om, {b, l});
+    at::Tensor i_out = view_of(st, at::kLong, oi, i.sizes());
+    at::Tensor done = view_of(st, at::kBool, od, {b, 1});
+    at::Tensor reward = view_of(st, at::kBool, orw, {b, 1});
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = fn(b, l, p, logits.const_data_ptr<float>(), logits.stride(0),
+            static_cast<const uint8_t*>(mask.const_data_ptr()), (float)clip, (float)temp, (int)mode,
+            ain ? ain->const_data_ptr<int64_t>() : nullptr, act.mutable_data_ptr<int64_t>(),
+            logp.mutable_data_ptr<float>(), seed, offset, tc.const_data_ptr<float>(), tc.stride(0),
+            asg.const_data_ptr<int32_t>(), asg_out.mutable_data_ptr<int32_t>(),
+            static_cast<uint8_t*>(mask_out.mutable_data_ptr()), i.const_data_ptr<int64_t>(),
+            i_out.mutable_data_ptr<int64_t>(), static_cast<uint8_t*>(done.mutable_data_ptr()),
+            static_cast<uint8_t*>(reward.mutable_data_ptr()), nullptr,
+            status.mutable_data_ptr<int32_t>(), stream);
+    Py_END_ALLOW_THREADS
+    if (rc != CO_OK) return PyLong_FromLong(rc);
+    PyObject* tc_next = THPVariable_Wrap(tc.slice(1, 1));  // to_choose[:, 1:] (a view)
+    if (!tc_next) return nullptr;
+    PyObject* res = td_finish(td, key, ain_o, act, logp,
+                              {{"assignment", &asg_out}, {"action_mask", &mask_out},
+                               {"i", &i_out}, {"reward", &reward}, {"done", &done}},
+                              {{"to_choose", tc_next}}, i_o, lb_attr, "i");
+    Py_DECREF(tc_next);
+    return res;
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// cvrp_step_td(fn, lb_attr, td, logits, mode, temp, clip, action_in, seed, offset, status,
+//              key) -> (action, logp) | None | error code
+// CVRPEnv.decode_and_step (envs/cvrp.py) on a dict-backed TensorDict in one call.
+PyObject* cvrp_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 12) {
+    PyErr_SetString(PyExc_TypeError, "cvrp_step_td: 12 arguments");
+    return nullptr;
+  }
+  PyObject* lb_attr = a[1];
+  PyObject* td = a[2];
+  PyObject* key = a[11];
+  PyObject* ain_o = a[7];
+  if (!PyDict_Check(td) || !is_tensor(a[3]) || !is_tensor(a[10]) ||
+      (ain_o != Py_None && !is_tensor(ain_o)) || !PyUnicode_Check(key) || !PyUnicode_Check(lb_attr))
+    Py_RETURN_NONE;
+  PyObject *mask_o = td_tensor(td, "action_mask"), *dem_o = td_tensor(td, "demand"),
+           *used_o = td_tensor(td, "used_capacity"), *cap_o = td_tensor(td, "vehicle_capacity"),
+           *vis_o = td_tensor(td, "visited");
+  if (!mask_o || !dem_o || !used_o || !cap_o || !vis_o) Py_RETURN_NONE;
+  const auto fn = fn_at<CvrpDecodeStep>(a[0]);
+  const long mode = PyLong_AsLong(a[4]);
+  const double temp = PyFloat_AsDouble(a[5]), clip = PyFloat_AsDouble(a[6]);
+  const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[8]);
+  const uint64_t offset = PyLong_AsUnsignedLongLongMask(a[9]);
+  if (PyErr_Occurred()) return nullptr;
+  try {
+    const at::Tensor& logits = THPVariable_Unpack(a[3]);
+    const at::Tensor& mask = THPVariable_Unpack(mask_o);
+    const at::Tensor& dem = THPVariable_Unpack(dem_o);
+    const at::Tensor& used = THPVariable_Unpack(used_o);
+    const at::Tensor& cap = THPVariable_Unpack(cap_o);
+    const at::Tensor& vis = THPVariable_Unpack(vis_o);
+    const at::Tensor& status = THPVariable_Unpack(a[10]);
+    const at::Tensor* ain = ain_o != Py_None ? &THPVariable_Unpack(ain_o) : nullptr;
+    const c10::Device dev = dem.device();
+    if (!dev.is_cuda() || dem.dim() != 2 || logits.device() != dev ||
+        logits.scalar_type() != at::kFloat || logits.dim() != 2 || logits.stride(1) != 1 ||
+        status.device() != dev || status.scalar_type() != at::kInt)
+      Py_RETURN_NONE;
+    const int64_t b = dem.size(0), nl = dem.size(1);
+    if (logits.size(0) != b || logits.size(1) != nl + 1 || nl + 1 > 2048 ||
+        !fits(dem, dev, at::kFloat) || !fits(used, dev, at::kFloat, b) ||
+        !fits(cap, dev, at::kFloat, b) || !fits(vis, dev, at::kByte, b * (nl + 1)) ||
+        !fits(mask, dev, at::kBool, b * (nl + 1)) || mask.dim() != 2)
+      Py_RETURN_NONE;
+    if (ain && !fits(*ain, dev, at::kLong, b)) Py_RETURN_NONE;
+    const int64_t kb = up(8 * b);
+    const int64_t ko = g_slab.take(dev, 2 * kb);
+    at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
+    at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b});
+    Carver c;
+    const int64_t ou = c.take(4 * b), ov = c.take(b * (nl + 1)), oc = c.take(8 * b),
+                  od = c.take(b), orw = c.take(b), om = c.take(b * (nl + 1));
+    void* stream = current_stream(dev);
+    const c10::Storage st = g_state.acquire(dev, c.off, stream);
+    at::Tensor used_out = view_of(st, at::kFloat, ou, used.sizes());
+    at::Tensor vis_out = view_of(st, at::kByte, ov, vis.sizes());
+    at::Tensor cur = view_of(st, at::kLong, oc, {b, 1});
+    at::Tensor done = view_of(st, at::kBool, od, {b});
+    at::Tensor reward = view_of(st, at::kBool, orw, {b});
+    at::Tensor mask_out = view_of(st, at::kBool, om, {b, nl + 1});
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = fn(b, nl, logits.const_data_ptr<float>(), logits.stride(0),
+            static_cast<const uint8_t*>(mask.const_data_ptr()), (float)clip, (float)temp, (int)mode,
+            ain ? ain->const_data_ptr<int64_t>() : nullptr, act.mutable_data_ptr<int64_t>(),
+            logp.mutable_data_ptr<float>(), seed, offset, dem.const_data_ptr<float>(),
+            used.const_data_ptr<float>(), used_out.mutable_data_ptr<float>(),
+            cap.const_data_ptr<float>(), vis.const_data_ptr<uint8_t>(),
+            vis_out.mutable_data_ptr<uint8_t>(), cur.mutable_data_ptr<int64_t>(),
+            static_cast<uint8_t*>(done.mutable_data_ptr()),
+            static_cast<uint8_t*>(reward.mutable_data_ptr()),
+            static_cast<uint8_t*>(mask_out.mutable_data_ptr()), nullptr,
+            status.mutable_data_ptr<int32_t>(), stream);
+    Py_END_ALLOW_THREADS
+    if (rc != CO_OK) return PyLong_FromLong(rc);
+    return td_finish(td, key, ain_o, act, logp,
+                     {{"current_node", &cur}, {"used_capacity", &used_out},
+                      {"visited", &vis_out}, {"reward", &reward}, {"done", &done},
+                      {"action_mask", &mask_out}},
+                     {}, vis_o, lb_attr, "visited");
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 // decode_step(fn, logits, mask, action_in, status, clip, temp, mode, seed, offset, full)
 //   -> (act, logp, full_logprobs | None) | None
 // fn: address of co_decode_step (utils/decoding.py:decode_step without top-k / top-p)
@@ -482,6 +708,10 @@ PyObject* clear_pool(PyObject*, PyObject* const*, Py_ssize_t) {
 }
 
 PyMethodDef methods[] = {
+    {"slap_step_td", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(slap_step_td)),
+     METH_FASTCALL, "SLAPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
+    {"cvrp_step_td", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(cvrp_step_td)),
+     METH_FASTCALL, "CVRPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
     {"clear_pool", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(clear_pool)),
      METH_FASTCALL, "drop the pooled step-state storages"},
     {"tsp_step_td", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(tsp_step_td)),

@@ -76,9 +76,6 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
 #define CO_TSP_STEP_GROUP 1
 #endif
 
-#ifndef CO_TSP_FLAT_ROWS
-#define CO_TSP_FLAT_ROWS 0  // rows per wave of the flat step kernel (0: the lane-group kernel)
-#endif
 #ifndef CO_TSP_WPL
 #define CO_TSP_WPL 4
 #endif
@@ -167,133 +164,6 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
       epi.store(r, a_raw, any_left ? 1 : 0, rv);
     }
   }
-}
-
-// Flat step (round 4): a wave owns R consecutive rows, i.e. the contiguous R*N mask bytes
-// [b0*N, (b0+R)*N) (16-byte aligned: R*N % 16 == 0 and an aligned base), moved as 16-byte
-// chunks -- lane l holds chunks l + 64u (u < CPL) -- so each load / store instruction
-// covers 1 KiB of the rows (the lane-group kernel's dword instructions: 256 B in 8 row
-// pieces), and the row scalars of the R rows are one coalesced access per column (lane r
-// owns row b0 + r).  A chunk holds bytes of at most two rows (N >= 16): r0 = 16j / N and
-// r1 = (16j + 15) / N; their actions come from the row lanes by ds_bpermute and clear the
-// chunk's byte of each (SWAR on the four words).  Row r's "anything left" is the OR of
-// its chunks' nonzero tests, evaluated on two ballots per chunk slot (f0: the chunk's
-// part in row r0, f1: the part in row r1): row r's first chunk contributes its f1 part
-// when it starts in row r - 1, the following ones their f0 part.  The last wave's
-// partial rows (B % R) leave a tail of < 16 bytes, moved as dwords (N % 4 == 0).
-template <int R, int CPL>
-__global__ __launch_bounds__(256) void tsp_step_flat_kernel(int64_t B, int N,
-                                                            const int64_t* __restrict__ action,
-                                                            const uint8_t* mask_in,
-                                                            uint8_t* mask_out, TspRowEpilogue epi,
-                                                            int first_mode,
-                                                            const int32_t* first_flag,
-                                                            int32_t* status) {
-  static_assert(R <= 64, "one row per lane for the row scalars");
-  const int lane = lane_id();
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int64_t b0 = wid * R;
-  if (b0 >= B) return;  // wave-uniform
-  if (first_mode == 2) epi.take_first = (*first_flag != 0);
-  const int rows = (int)(B - b0 < R ? B - b0 : R);
-  const int nbytes = rows * N, nch = nbytes >> 4;
-  // row scalars: lane r < rows owns row b0 + r (coalesced)
-  const bool rl = lane < rows;
-  const int64_t rb = b0 + (rl ? lane : 0);
-  const int64_t a_raw = rl ? action[rb] : 0;
-  int64_t iv = 0, fv = 0;
-  if (rl) {
-    iv = epi.i_in[rb];
-    if (!epi.take_first) fv = epi.first_in[rb];
-  }
-  const uint4* src = reinterpret_cast<const uint4*>(mask_in + b0 * N);
-  uint4 m[CPL];
-#pragma unroll
-  for (int u = 0; u < CPL; ++u) {
-    const int j = lane + 64 * u;
-    m[u] = j < nch ? src[j] : make_uint4(0u, 0u, 0u, 0u);
-  }
-  // tail dwords of a partial last wave (nbytes % 16 != 0)
-  const int ntail = (nbytes & 15) >> 2;
-  const uint32_t* srcw = reinterpret_cast<const uint32_t*>(mask_in + b0 * N) + 4 * nch;
-  uint32_t tw = lane < ntail ? srcw[lane] : 0u;
-  const bool bad = rl && (a_raw < 0 || a_raw >= N);
-  if (bad) set_status(status, CO_ST_INDEX_RANGE);
-  const int a32 = bad ? -1 : (int)a_raw;  // the row's action (-1: clears nothing)
-  uint64_t B0[CPL], B1[CPL];
-#pragma unroll
-  for (int u = 0; u < CPL; ++u) {
-    const int j = lane + 64 * u;
-    const int o = 16 * j;                       // the chunk's first byte (wave-relative)
-    const int r0 = o / N, r1 = (o + 15) / N;    // its rows (r1 <= r0 + 1 for N >= 16)
-    const int a0 = __shfl(a32, r0 < 64 ? r0 : 63, 64), a1 = __shfl(a32, r1 < 64 ? r1 : 63, 64);
-    const int p0 = a0 < 0 ? -1 : r0 * N + a0 - o, p1 = a1 < 0 ? -1 : r1 * N + a1 - o;
-    uint32_t w[4] = {m[u].x, m[u].y, m[u].z, m[u].w};
-    const int split = r1 == r0 ? 16 : r1 * N - o;  // first byte of row r1 in the chunk
-    bool f0 = false, f1 = false;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t x = w[q];
-      if ((unsigned)(p0 - 4 * q) < 4u) x &= ~(0xffu << (8 * (p0 - 4 * q)));
-      if ((unsigned)(p1 - 4 * q) < 4u) x &= ~(0xffu << (8 * (p1 - 4 * q)));
-      w[q] = x;
-      const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
-      // bytes 4q + e (high bit of byte e of nz) before / at-or-after the row split
-      const int lo = split - 4 * q;  // bytes e < lo belong to row r0
-      const uint32_t below = lo <= 0 ? 0u : (lo >= 4 ? 0xffffffffu : (1u << (8 * lo)) - 1u);
-      f0 |= (nz & below) != 0u;
-      f1 |= (nz & ~below) != 0u;
-    }
-    m[u] = make_uint4(w[0], w[1], w[2], w[3]);
-    const bool live = j < nch;
-    B0[u] = __ballot(live && f0);
-    B1[u] = __ballot(live && f1 && r1 != r0);
-  }
-  uint4* dst = reinterpret_cast<uint4*>(mask_out + b0 * N);
-#pragma unroll
-  for (int u = 0; u < CPL; ++u) {
-    const int j = lane + 64 * u;
-    if (j < nch) dst[j] = m[u];
-  }
-  // the tail dwords: row of byte 4*(4*nch + lane) and its action
-  bool tail_nz = false;
-  int tail_row = 0;
-  if (ntail) {
-    const int o = 16 * nch + 4 * lane;
-    tail_row = o / N;
-    const int at = __shfl(a32, tail_row < 64 ? tail_row : 63, 64);
-    const int pt = at < 0 ? -1 : tail_row * N + at - o;
-    if ((unsigned)pt < 4u) tw &= ~(0xffu << (8 * pt));
-    tail_nz = lane < ntail && tw != 0u;
-    if (lane < ntail) reinterpret_cast<uint32_t*>(mask_out + b0 * N)[4 * nch + lane] = tw;
-  }
-  const uint64_t BT = __ballot(tail_nz);
-  if (!rl) return;
-  // row lane r: its chunks jlo..jhi (and tail dwords past the last whole chunk)
-  const int r = lane;
-  const int first_b = r * N, last_b = r * N + N - 1;
-  const int jlo = first_b >> 4, jhi = last_b >> 4;
-  bool left = false;
-#pragma unroll
-  for (int u = 0; u < CPL; ++u) {
-    // chunk j = 64u + bit: f1 part for jlo when it starts in row r - 1, else f0 parts
-    const int lo = jlo - 64 * u, hi = (jhi < nch - 1 ? jhi : nch - 1) - 64 * u;
-    const int lo0 = ((jlo << 4) < first_b ? jlo + 1 : jlo) - 64 * u;
-    auto range = [](int a, int b) -> uint64_t {  // bits a..b of a 64-bit word (clamped)
-      a = a < 0 ? 0 : a;
-      b = b > 63 ? 63 : b;
-      if (a > b) return 0ull;
-      const uint64_t hi_m = b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
-      return hi_m & ~((1ull << a) - 1ull);
-    };
-    left |= (B0[u] & range(lo0, hi)) != 0ull;
-    if ((jlo << 4) < first_b) left |= (B1[u] & range(lo, lo)) != 0ull;
-  }
-  if (ntail) {  // tail dwords t: byte offset 16*nch + 4t, row (16*nch + 4t) / N
-    const int t_lo = (first_b - 16 * nch) >> 2, t_hi = (last_b - 16 * nch) >> 2;
-    for (int t = t_lo < 0 ? 0 : t_lo; t <= t_hi && t < ntail; ++t) left |= (BT >> t) & 1ull;
-  }
-  epi.store(rb, a_raw, left ? 1 : 0, TspRowEpilogue::Row{iv, fv});
 }
 
 template <int WAVES>
@@ -401,25 +271,6 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
   const int vec = tile_vec_ok(mask_in, mask_out);
   TspRowEpilogue epi{i_in, i_out, first_in, first_out, current_out, done, reward,
                      first_mode == 1};
-  // flat step: R rows per wave as 16-byte chunks (N % 4 == 0, 16 <= N, R*N % 16 == 0,
-  // 16-byte aligned masks, at most 4 chunks per lane)
-  constexpr int FR = CO_TSP_FLAT_ROWS;
-  if (FR > 0 && (N & 3) == 0 && N >= 16 && (FR * N) % 16 == 0 && (FR * N + 1023) / 1024 <= 4 &&
-      ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) & 15) == 0) {
-    const int cpl = (int)((FR * N / 16 + 63) / 64);
-    const int64_t waves = (B + FR - 1) / FR;
-    const dim3 grid((unsigned)((waves + 3) / 4));
-    hipStream_t s = (hipStream_t)stream;
-#define CO_TSF(C)                                                                              \
-  hipLaunchKernelGGL((tsp_step_flat_kernel<FR, C>), grid, dim3(256), 0, s, B, (int)N, action,   \
-                     mask_in, mask_out, epi, first_mode, first_flag, status)
-    if (cpl <= 1) CO_TSF(1);
-    else if (cpl == 2) CO_TSF(2);
-    else if (cpl == 3) CO_TSF(3);
-    else CO_TSF(4);
-#undef CO_TSF
-    return launch_status();
-  }
   if (CO_TSP_STEP_GROUP && (N & 3) == 0 && (N >> 2) <= 64 * CO_TSP_WPL &&
       ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) & 3) == 0) {
     const int W = (int)(N >> 2), WG = (W + CO_TSP_WPL - 1) / CO_TSP_WPL;

@@ -149,6 +149,19 @@ class CVRPEnv(RL4COEnvBase):
                       "reward": reward, "done": done, "action_mask": mask})
         return td
 
+    def native_decode_and_step(self):
+        """``decode_and_step``'s native call for a decoding strategy's loop (the step glue
+        ``csrc/pycall/co_torchstep.cpp``: cvrp_step_td): ``f(td, logits, mode, temperature,
+        tanh_clipping, action_in, seed, offset, status, key)`` returning ``(action, logp)``,
+        an error code, or None (then call ``decode_and_step``); None when the glue is
+        unavailable."""
+        ts = nat.torchstep()
+        if ts is None:
+            return None
+        import functools
+
+        return functools.partial(ts.cvrp_step_td, self._lb_attr)
+
     def decode_and_step(self, td, logits, mode, temperature, tanh_clipping, action_in, seed,
                         offset, status, key="action"):
         """``DecodingStrategy.step`` + ``_step`` (``decoding.py:327-369``,

@@ -184,6 +184,17 @@ def _cvrp_pair(b, n, dev, seed=5):
     return gen, env
 
 
+def _count_fused_calls(monkeypatch, env, calls):
+    """Count the fused decode + env steps, whichever form runs: the native step glue
+    (``native_decode_and_step``) or the Python ``decode_and_step``."""
+    real = env.decode_and_step
+    monkeypatch.setattr(env, "decode_and_step", lambda *a, **k: calls.append(1) or real(*a, **k))
+    native = env.native_decode_and_step()
+    if native is not None:
+        counted = lambda *a, **k: calls.append(1) or native(*a, **k)  # noqa: E731
+        monkeypatch.setattr(env, "native_decode_and_step", lambda: counted)
+
+
 @pytest.mark.parametrize("name", ["slap", "cvrp"])
 @pytest.mark.parametrize("decode_type", ["greedy", "sampling", "multistart_greedy", "evaluate"])
 @pytest.mark.parametrize("math", ["certified", "exact"])
@@ -217,9 +228,7 @@ def test_fused_decode_env_step_equals_two_launches(dev, monkeypatch, name, decod
         td = env.reset(TensorDict({k: v.clone().to(dev) for k, v in gen.items()}, [b]))
         pol = ConstructivePolicy(None, dec, env_name=name, tanh_clipping=10.0)
         calls = []
-        real = env.decode_and_step
-        monkeypatch.setattr(env, "decode_and_step",
-                            lambda *a, **k: calls.append(1) or real(*a, **k))
+        _count_fused_calls(monkeypatch, env, calls)
         torch.manual_seed(123)
         if decode_type == "evaluate":
             kw = {"actions": acts}
@@ -309,3 +318,39 @@ def test_fused_cvrp_decode_step_kernel_matches_two_launches_direct(dev):
             for x, y in zip(o1, o2):
                 assert torch.equal(x, y), (b, n, mode)
             assert int(st1.item()) == int(st2.item()), (b, n, mode)
+
+
+@pytest.mark.parametrize("name", ["slap", "cvrp"])
+@pytest.mark.parametrize("decode_type", ["greedy", "sampling"])
+def test_native_step_glue_equals_python_fused_path(dev, monkeypatch, name, decode_type):
+    """The step glue (csrc/pycall/co_torchstep.cpp slap_step_td / cvrp_step_td) and the
+    Python decode_and_step launch the same kernel on the same state: same actions, logp,
+    reward and final state; the done-poll lower bound recorded on the new state."""
+    b = 33
+    if name == "slap":
+        gen = _slap_instance(b, 21)
+        dec = SLAPPointerDecoder(gen["locs"], dev)
+        keys = ("assignment", "action_mask", "i", "done", "to_choose")
+    else:
+        gen, _ = _cvrp_pair(b, 23, dev, seed=8)
+        dec = PointerDecoder(torch.cat((gen["depot"][:, None], gen["locs"]), 1), dev,
+                             depot_env=True)
+        keys = ("action_mask", "visited", "used_capacity", "current_node", "done")
+    outs = []
+    for native in (True, False):
+        env = (SLAPEnv(device=dev) if name == "slap"
+               else CVRPEnv(generator_params=dict(num_loc=23), device=dev))
+        if not native:
+            monkeypatch.setattr(env, "native_decode_and_step", lambda: None)
+        elif env.native_decode_and_step() is None:
+            pytest.skip("step glue not built for this torch / interpreter")
+        td = env.reset(TensorDict({k: v.clone().to(dev) for k, v in gen.items()}, [b]))
+        pol = ConstructivePolicy(None, dec, env_name=name, tanh_clipping=10.0)
+        torch.manual_seed(5)
+        outs.append((pol(td, env, phase="test", decode_type=decode_type, return_actions=True),
+                     {k: td[k].clone() for k in keys}))
+    (a, sa), (b_, sb) = outs
+    for k in ("actions", "log_likelihood", "reward"):
+        assert torch.equal(a[k], b_[k]), k
+    for k in keys:
+        assert torch.equal(sa[k], sb[k]), k
