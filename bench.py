@@ -1026,8 +1026,25 @@ def bench_dropin_slap(b, k, world, rank, dev):
                 out[key + "host_us_per_step_b64"] = t / kk / P * 1e6
             env.decode_and_step, env.native_decode_and_step = real
             del env, pol, dec, data
+    # the marginal host cost of one loop step: episodes of P = 20 and 40 products at B = 64
+    # (the per-episode reset / reward / log-likelihood / status read cancel out)
+    te = {}
+    for pp in (P, 2 * P):
+        torch.manual_seed(1234 + rank)
+        np.random.seed(1234 + rank)
+        data = SLAPGenerator(n_products=pp, materialize_dist_mat=False)(64).to(dev)
+        logits = torch.randn(64, data["locs"].shape[1],
+                             generator=torch.Generator().manual_seed(11)).to(dev)
+        env = SLAPEnv(device=dev)
+        pol = ConstructivePolicy(None, LogitsDecoder(lambda td, lg=logits: lg), env_name="slap",
+                                 tanh_clipping=10.0)
+        run = lambda: pol(env.reset(TensorDict(dict(data.items()), [64])), env,  # noqa: E731
+                          phase="test", decode_type="greedy")
+        wall, _ = timed(run, 3 * k, 2, world, dev)
+        te[pp] = max_over_ranks(wall, world, dev) / (3 * k)
+    out["host_us_per_loop_step_b64"] = (te[2 * P] - te[P]) / P * 1e6
     out["decode_fused_kernel_us"] = slap_decode_step_kernel_us(b, dev)
-    out["host_below_kernel"] = out["host_us_per_step_b64"] < out["decode_fused_kernel_us"]
+    out["host_below_kernel"] = out["host_us_per_loop_step_b64"] < out["decode_fused_kernel_us"]
     # the SLAP step 2L+34 B + the decode's logits 4L + logp 4 per env-step
     out["bytes_per_env_step"] = 2 * 100 + 34 + 4 * 100 + 4
     return out

@@ -593,12 +593,22 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
     L = g.template softmax_shift<OF>(clip, temp, N, sl, lds_row);
     int sel = g.select(L, c0, lp);
     const bool ok = !valid || g.template certify<OF>(L, sel, c0, N, clip, temp);
+#if defined(CO_DIAG_CERT_NOFALLBACK)  // timing diagnostics only: no fallback code at all /
+    if (false) {                          // the fallback compiled in but never taken
+#elif defined(CO_DIAG_CERT_NEVER)
+    if (__any(!ok) && N < 0) {
+#else
     if (__any(!ok)) {  // rare: the exact evaluation for the whole wave
+#endif
+
       // the raw row is read again (an L2 hit) rather than kept in EPL registers through
       // the fast path: the kernel's VGPR count is the fast path's
       g.load(valid, N, lrow, mrow, c0);
       L = g.template softmax_shift<OE, false>(clip, temp, N, sl, lds_row);
       sel = g.select(L, c0, lp);
+#ifdef CO_DIAG_CERT_COUNT  // diagnostic only: marks the rows of waves that fell back
+      lp = -12345.f;
+#endif
     }
     return sel;
   } else {

@@ -425,6 +425,7 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
            *fr_o = td_tensor(td, "freq");
   if (!mask_o || !i_o || !tc_o || !as_o || !fr_o) Py_RETURN_NONE;
   const auto fn = fn_at<SlapDecodeStep>(a[0]);
+  const long long ki = known(i_o, g_attr_i);
   const long mode = PyLong_AsLong(a[4]);
   const double temp = PyFloat_AsDouble(a[5]), clip = PyFloat_AsDouble(a[6]);
   const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[8]);
@@ -488,6 +489,17 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
                                {"i", &i_out}, {"reward", &reward}, {"done", &done}},
                               {{"to_choose", tc_next}}, i_o, lb_attr, "i");
     Py_DECREF(tc_next);
+    // i is uniform over the batch when the env knows its value (reset: 0; every step +1)
+    // and done = (i == P-1) then is too: the records let poll_done answer without a read
+    if (res && ki >= 0) {
+      PyObject* i_n = PyDict_GetItemString(td, "i");
+      PyObject* d_n = PyDict_GetItemString(td, "done");
+      if (!i_n || !d_n || remember(i_n, g_attr_i, ki + 1) ||
+          remember(d_n, g_attr_i, ki == p - 1 ? 1 : 0)) {
+        Py_DECREF(res);
+        return nullptr;
+      }
+    }
     return res;
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());

@@ -603,8 +603,8 @@ __device__ __forceinline__ int slap_pick_loc(int pp, const int32_t* asg, int L, 
   }
   return (int)loc;
 }
-template <int KU>
-__device__ __forceinline__ float slap_order_len(const int32_t* pk, const int32_t* asg,
+template <int KU, typename PK>
+__device__ __forceinline__ float slap_order_len(const PK* pk, const int32_t* asg,
                                                 const float2* xy, int L, bool& range,
                                                 int K = KU) {
   int pp[KU], lc[KU];
@@ -630,9 +630,14 @@ __host__ __device__ inline size_t slap_asg_bytes(int ipb, int P) {
 }
 __host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O, int K) {
   const size_t keys = (size_t)epl * 64 * 8;
-  const size_t data = (size_t)gpw * (L * 8 + O * 4 + O * K * 4);
+  // coordinates f32x2, order lengths f32, picklist products int16 (P <= 4,096)
+  const size_t data = (size_t)gpw * (L * 8 + O * 4 + O * K * 2);
   return ((keys > data ? keys : data) + 15) & ~(size_t)15;
 }
+
+#ifndef CO_SLAP_LATE
+#define CO_SLAP_LATE 0  // 1: the coordinates, 2: also the picklist loaded after the step loop
+#endif
 
 template <int G, int EPL, bool CLOSEST>
 __global__ __launch_bounds__(256) void slap_group_kernel(
@@ -659,7 +664,7 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
   float2* xy = reinterpret_cast<float2*>(wreg) + gw * L;
   int32_t* asg = s_asg + g * P;
   float* olen = reinterpret_cast<float*>(wreg + (size_t)GPW * L * 8) + gw * O;
-  int32_t* pks = reinterpret_cast<int32_t*>(wreg + (size_t)GPW * (L * 8 + O * 4)) + gw * O * K;
+  int16_t* pks = reinterpret_cast<int16_t*>(wreg + (size_t)GPW * (L * 8 + O * 4)) + gw * O * K;
 
   // Loads are issued in the order they are needed: the depot distances (the step loop),
   // then the coordinates and up to G*EPL picklist entries, which stay in registers during
@@ -685,8 +690,12 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
     const int c = sl + G * k;
+#if !CO_SLAP_LATE
     xr[k] = c < L ? lrow[c] : make_float2(0.f, 0.f);
+#endif
+#if CO_SLAP_LATE < 2
     pr[k] = c < O * K ? prow[c] : 0;
+#endif
   }
   // closest-free = the free locations in increasing (distance, index) order.  Each lane
   // sorts its EPL candidates once (keys: order-preserving u32 of the distance, then the
@@ -700,8 +709,10 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
     return (pp < 0 || pp >= P) ? -1 : (int32_t)pp;
   };
   int32_t pw[EPL];
+#if CO_SLAP_LATE < 2
 #pragma unroll
   for (int k = 0; k < EPL; ++k) pw[k] = wrap_product(pr[k]);
+#endif
   uint64_t key[EPL];
   if (CLOSEST) {
 #pragma unroll
@@ -794,15 +805,25 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
     const int c = sl + G * k;
+#if CO_SLAP_LATE
+    xr[k] = c < L ? lrow[c] : make_float2(0.f, 0.f);
+#endif
     if (c < L) xy[c] = xr[k];
   }
   // picklist entries as wrapped product indices (-1 = out of range)
+#if CO_SLAP_LATE >= 2
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const int c = sl + G * k;
+    pw[k] = c < O * K ? wrap_product(prow[c]) : 0;
+  }
+#endif
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {  // entry sl + G*k is register pw[k]
     const int c = sl + G * k;
-    if (c < O * K) pks[c] = pw[k];
+    if (c < O * K) pks[c] = (int16_t)pw[k];
   }
-  for (int c = sl + G * EPL; c < O * K; c += G) pks[c] = wrap_product(prow[c]);
+  for (int c = sl + G * EPL; c < O * K; c += G) pks[c] = (int16_t)wrap_product(prow[c]);
   // the group's LDS rows are written and read by lanes of the same wave: a wave-level
   // fence orders them, no workgroup barrier (groups do not wait for other waves)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -824,7 +845,7 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
   // one lane per order; for K <= 8 the K picks' LDS lookups (product -> location ->
   // coordinates) are three independent batches, not a K-long dependent chain
   for (int o = sl; o < O; o += G) {
-    const int32_t* pk = pks + o * K;
+    const int16_t* pk = pks + o * K;
     float len = 0.f;
     if (K == 5) {  // examples/slap.py: max_products_in_order = 5
       len = slap_order_len<5>(pk, asg, xy, L, range);
@@ -860,6 +881,8 @@ __global__ __launch_bounds__(256) void slap_group_kernel(
       const int c = sl + G * k;
       if (c < L) mrow[c] = (avail >> k) & 1u;
     }
+    // (not unrolled: the compiler's 16-way unroll of this loop set the kernel's VGPR peak)
+#pragma unroll 2
     for (int c = sl; c < P; c += G) assign_out[bb * P + c] = asg[c];
     if (sl == 0) {
       // f32 order-by-order accumulation of slap/env.py:135-142

@@ -86,6 +86,10 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
 #define CO_TSP_SCUT 0  // timing diagnostic only: 1 no row epilogue, 2 no mask store
 #endif
 
+#ifndef CO_TSP_UNR
+#define CO_TSP_UNR 1  // row groups per wave (all their loads issued before the first use)
+#endif
+
 template <int G>
 __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
                                                              const int64_t* __restrict__ action,
@@ -94,44 +98,53 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
                                                              TspRowEpilogue epi, int first_mode,
                                                              const int32_t* first_flag,
                                                              int32_t* status) {
-  constexpr int WPL = CO_TSP_WPL;
+  constexpr int WPL = CO_TSP_WPL, U = CO_TSP_UNR;
   const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
   const int W = N >> 2;  // words per row
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
   if (first_mode == 2) epi.take_first = (*first_flag != 0);
-  // one row group per wave (the grid covers B; no grid-stride loop)
-  const int64_t base = wid * (64 / G);
+  // U row groups per wave (the grid covers B; no grid-stride loop)
+  const int64_t base = wid * (64 / G) * U;
   if (base >= B) return;  // wave-uniform
-  {
-    const int64_t b = base + lane / G;
-    const bool valid = b < B;
-    const int64_t r = valid ? b : 0;
-    const int64_t a_raw = action[r];
-    int64_t a = a_raw;
+  int64_t rr[U], a_raw[U], rs[U];
+  bool valid[U];
+  uint32_t w[U][WPL];
+  typename TspRowEpilogue::Row rv[U];
+  // CO_TSP_LAYOUT 1: word c = sl + k*G (each load/store instruction covers G consecutive
+  // words of a row); 0: c = sl*WPL + k (a lane's words adjacent)
+#define CO_TSP_WORD(k) (CO_TSP_LAYOUT ? sl + (k) * G : sl * WPL + (k))
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t b = base + u * (64 / G) + lane / G;
+    valid[u] = b < B;
+    const int64_t r = rr[u] = valid[u] ? b : 0;
+    a_raw[u] = action[r];
     // row scalars: with G >= 8 spread over the group's lanes (lane 0 reads i, lane 1
     // first_node: one load instruction; lanes 0-2 write i / first / current: one 8-B
     // store; lanes 3, 4 done / reward: one byte store), else lane 0 does all of them
-    typename TspRowEpilogue::Row rv{};
-    int64_t rs = 0;
+    rv[u] = {};
+    rs[u] = 0;
     if constexpr (G >= 8) {
       const int64_t* rsrc = sl == 0 ? epi.i_in : epi.first_in;
-      if (valid && (sl == 0 || (sl == 1 && !epi.take_first)) && !(CO_TSP_SCUT & 1)) rs = rsrc[r];
-    } else if (valid && !(CO_TSP_SCUT & 1)) {
-      rv = epi.load(r);
+      if (valid[u] && (sl == 0 || (sl == 1 && !epi.take_first)) && !(CO_TSP_SCUT & 1))
+        rs[u] = rsrc[r];
+    } else if (valid[u] && !(CO_TSP_SCUT & 1)) {
+      rv[u] = epi.load(r);
     }
     const uint32_t* src = mask_in + r * W;
-    uint32_t w[WPL];
-    // CO_TSP_LAYOUT 1: word c = sl + k*G (each load/store instruction covers G consecutive
-    // words of a row); 0: c = sl*WPL + k (a lane's words adjacent)
-#define CO_TSP_WORD(k) (CO_TSP_LAYOUT ? sl + (k) * G : sl * WPL + (k))
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
       const int c = CO_TSP_WORD(k);
-      w[k] = (valid && c < W) ? src[c] : 0u;
+      w[u][k] = (valid[u] && c < W) ? src[c] : 0u;
     }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t r = rr[u];
+    int64_t a = a_raw[u];
     if (a < 0 || a >= N) {
-      if (valid && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
+      if (valid[u] && sl == 0) set_status(status, CO_ST_INDEX_RANGE);
       a = -1;
     }
     const int aw = a >= 0 ? (int)(a >> 2) : -1;  // the action's word and byte
@@ -140,30 +153,30 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
       const uint32_t clr = CO_TSP_WORD(k) == aw ? aclr : 0u;
-      w[k] &= ~clr;
+      w[u][k] &= ~clr;
       // nonzero bytes of the word: high bit of each byte of (b & 0x7f) + 0x7f, or b
-      const uint32_t nz = (((w[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[k]) & 0x80808080u;
+      const uint32_t nz = (((w[u][k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[u][k]) & 0x80808080u;
       left += __builtin_popcount(nz);
     }
     uint32_t* dst = mask_out + r * W;
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
       const int c = CO_TSP_WORD(k);
-      if (valid && c < W && !(CO_TSP_SCUT & 2)) dst[c] = w[k];
+      if (valid[u] && c < W && !(CO_TSP_SCUT & 2)) dst[c] = w[u][k];
     }
-#undef CO_TSP_WORD
     const bool any_left = (__ballot(left != 0) & gmask) != 0;
     if constexpr (G >= 8) {
-      if (valid && !(CO_TSP_SCUT & 1)) {
+      if (valid[u] && !(CO_TSP_SCUT & 1)) {
         int64_t* d8 = sl == 0 ? epi.i_out : sl == 1 ? epi.first_out : epi.cur_out;
-        const int64_t v8 = sl == 0 ? rs + 1 : (sl == 1 && !epi.take_first) ? rs : a_raw;
+        const int64_t v8 = sl == 0 ? rs[u] + 1 : (sl == 1 && !epi.take_first) ? rs[u] : a_raw[u];
         if (sl < 3 && d8) d8[r] = v8;
         if (sl == 3 || sl == 4) (sl == 3 ? epi.done : epi.reward)[r] = sl == 3 ? !any_left : 0;
       }
-    } else if (valid && sl == 0 && !(CO_TSP_SCUT & 1)) {
-      epi.store(r, a_raw, any_left ? 1 : 0, rv);
+    } else if (valid[u] && sl == 0 && !(CO_TSP_SCUT & 1)) {
+      epi.store(r, a_raw[u], any_left ? 1 : 0, rv[u]);
     }
   }
+#undef CO_TSP_WORD
 }
 
 template <int WAVES>
@@ -275,8 +288,8 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
       ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) & 3) == 0) {
     const int W = (int)(N >> 2), WG = (W + CO_TSP_WPL - 1) / CO_TSP_WPL;
     const int G = WG <= 2 ? 2 : WG <= 4 ? 4 : WG <= 8 ? 8 : WG <= 16 ? 16 : WG <= 32 ? 32 : 64;
-    const int64_t waves = (B * G + 63) / 64;
-    const dim3 grid(grid_for(waves, 4, (int64_t)1 << 30));  // a wave per row group
+    const int64_t waves = (B * G + 64 * CO_TSP_UNR - 1) / (64 * CO_TSP_UNR);
+    const dim3 grid(grid_for(waves, 4, (int64_t)1 << 30));  // a wave per CO_TSP_UNR row groups
     const uint32_t* mi = reinterpret_cast<const uint32_t*>(mask_in);
     uint32_t* mo = reinterpret_cast<uint32_t*>(mask_out);
     hipStream_t s = (hipStream_t)stream;

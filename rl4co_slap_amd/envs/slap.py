@@ -131,6 +131,7 @@ class SLAPEnv(RL4COEnvBase):
         nat.call("co_slap_reset", b, l, p, nat.ptr(mask), nat.ptr(to_choose), nat.ptr(i),
                  nat.ptr(reward), nat.ptr(ratio), nat.stream_of(assignment))
         self._remember_lb(i, p)  # done = (i == P-1) before the step (slap/env.py:57)
+        self._remember_i(i, 0)
         return TensorDict({"assignment": assignment, "to_choose": to_choose, "i": i,
                            "ratio": ratio, "action_mask": mask, "reward": reward},
                           batch_size=batch_size)
@@ -156,12 +157,32 @@ class SLAPEnv(RL4COEnvBase):
         nat.call("co_slap_step", b, l, p, nat.ptr(action), nat.ptr(tc), tc.stride(0),
                  nat.ptr(assign), nat.ptr(assign_out), nat.ptr(mask), nat.ptr(mask_out),
                  nat.ptr(i), nat.ptr(i_out), nat.ptr(done), nat.ptr(reward), None, s)
-        lb = self._known_lb(td["i"])
-        if lb is not None:
-            self._remember_lb(i_out, lb - 1)
+        self._step_records(td["i"], i_out, done, p)
         td.update({"assignment": assign_out, "to_choose": tc[..., 1:], "action_mask": mask_out,
                    "i": i_out, "reward": reward, "done": done})
         return td
+
+    def _step_records(self, i_in, i_out, done, p):
+        """Host-side knowledge carried to a step's outputs: the done lower bound, and --
+        when every entry of ``i`` is known to hold one value (reset: 0; each step adds 1
+        to every row, ``slap/env.py:57-58``) -- that value, and then ``done = (i == P-1)``
+        is uniform too (recorded on ``done``: ``poll_done`` answers without a read)."""
+        lb = self._known_lb(i_in)
+        if lb is not None:
+            self._remember_lb(i_out, lb - 1)
+        k = self._known_i(i_in)
+        if k is not None:
+            self._remember_i(i_out, k + 1)
+            self._remember_i(done, int(k == p - 1))
+
+    def poll_done(self, td):
+        """``td["done"].all()``: known on the host when the step that produced ``done``
+        knew ``i`` (see ``_step_records``), else one device read."""
+        d = td.get_raw("done") if hasattr(td, "get_raw") else td["done"]
+        k = self._known_i(d) if isinstance(d, torch.Tensor) else None
+        if k is not None:
+            return bool(k), 1
+        return super().poll_done(td)
 
     def native_decode_and_step(self):
         """``decode_and_step``'s native call for a decoding strategy's loop (the step glue
@@ -211,9 +232,7 @@ class SLAPEnv(RL4COEnvBase):
                  nat.ptr(logp), seed, offset, nat.ptr(tc), tc.stride(0), nat.ptr(assign),
                  nat.ptr(assign_out), nat.ptr(mask_out), nat.ptr(i), nat.ptr(i_out),
                  nat.ptr(done), nat.ptr(reward), None, nat.ptr(status), s)
-        lb = self._known_lb(td["i"])
-        if lb is not None:
-            self._remember_lb(i_out, lb - 1)
+        self._step_records(td["i"], i_out, done, p)
         sel = action_in if action_in is not None else act
         set_many(td, {key: sel, "assignment": assign_out, "to_choose": tc[..., 1:],
                       "action_mask": mask_out, "i": i_out, "reward": reward, "done": done})

@@ -26,6 +26,7 @@ from oracle.rollout import constructive_forward
 from oracle.td import TD
 from rl4co_slap_amd import TensorDict
 from rl4co_slap_amd.envs import CVRPEnv, SLAPEnv
+from rl4co_slap_amd.envs.base import RL4COEnvBase
 from rl4co_slap_amd.envs.slap import SLAPGenerator
 from rl4co_slap_amd.rollout import ConstructivePolicy, LogitsDecoder
 
@@ -337,6 +338,10 @@ def test_native_step_glue_equals_python_fused_path(dev, monkeypatch, name, decod
                              depot_env=True)
         keys = ("action_mask", "visited", "used_capacity", "current_node", "done")
     outs = []
+    reads = []
+    base_poll = RL4COEnvBase.poll_done
+    monkeypatch.setattr(RL4COEnvBase, "poll_done",
+                        lambda self, td: reads.append(1) or base_poll(self, td))
     for native in (True, False):
         env = (SLAPEnv(device=dev) if name == "slap"
                else CVRPEnv(generator_params=dict(num_loc=23), device=dev))
@@ -349,6 +354,8 @@ def test_native_step_glue_equals_python_fused_path(dev, monkeypatch, name, decod
         torch.manual_seed(5)
         outs.append((pol(td, env, phase="test", decode_type=decode_type, return_actions=True),
                      {k: td[k].clone() for k in keys}))
+        if name == "slap":  # done known on the host (uniform i): the loop's poll reads nothing
+            assert env._known_i(td["done"]) == 1 and not reads
     (a, sa), (b_, sb) = outs
     for k in ("actions", "log_likelihood", "reward"):
         assert torch.equal(a[k], b_[k]), k

@@ -109,6 +109,33 @@ def test_slap_cpu_closest_episode():
     _close(r, r_ref)
 
 
+def test_slap_poll_done_known_on_host_matches_device_done():
+    """SLAPEnv.poll_done answers from the host records (i uniform from reset, +1 a step)
+    exactly when done.all() would; an in-place edit of done or a td without the records
+    falls back to the read."""
+    b = 16
+    ref_env = SLAPOracle(seed=3)
+    np.random.seed(3)
+    gen = ref_env.generate([b])
+    env = SLAPEnv(device="cpu")
+    td = env.reset(TensorDict({k: v.clone() for k, v in gen.items()}, [b]))
+    p = gen["freq"].shape[-2]
+    reads = []
+    real = SLAPEnv.__mro__[1].poll_done
+    for s in range(p):
+        free = (~td["action_mask"]).nonzero()
+        td.set("action", torch.stack([free[free[:, 0] == r][0, 1] for r in range(b)]))
+        td = env.step(td)["next"]
+        d = td["done"]
+        assert env._known_i(d) == int(s == p - 1)
+        assert env.poll_done(td) == (bool(d.all()), 1)
+    d = td["done"]
+    d[0] = False  # an in-place edit: the record goes stale, the poll reads the tensor
+    assert env._known_i(d) is None
+    reads.append(real(env, td))
+    assert env.poll_done(td) == reads[-1] == (False, 1)
+
+
 @pytest.mark.parametrize("clip", [0.0, 10.0])
 @pytest.mark.parametrize("temp", [1.0, 0.7])
 @pytest.mark.parametrize("n", [7, 20, 100])

@@ -66,6 +66,8 @@ def main():
         out = bench.bench_dropin(65536, 100, a.k, 1, 0, dev)
     elif a.mode == "dropin_cvrp":
         out = bench.bench_dropin_cvrp(32768, 100, a.k, 1, 0, dev)
+    elif a.mode == "dropin_slap":
+        out = bench.bench_dropin_slap(16384, a.k, 1, 0, dev)
     elif a.mode == "pomo":
         out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev)
     elif a.mode == "pomo_cert":
