@@ -502,6 +502,19 @@ struct GreedyRow {
     wave_tanh_compact<EPL>(v, ok, wave_lds);
   }
 
+  // the processed logit z of a raw logit x (softmax_shift's arithmetic, in its order):
+  // clip * tanh(x), then / temp; z_scale: the same from an already computed tanh
+  template <int OPT>
+  static __device__ __forceinline__ float z_scale(float t, float clip, float temp) {
+    if (OPT & kOptClip) t = t * clip;
+    if (OPT & kOptTemp) t = t / temp;
+    return t;
+  }
+  template <int OPT>
+  static __device__ __forceinline__ float z_of(float x, float clip, float temp) {
+    return z_scale<OPT>((OPT & kOptClip) ? clip_tanh<OPT>(x) : x, clip, temp);
+  }
+
   // COMPACT = false: the certified path's rare exact fallback (the compaction there made
   // the whole certified kernel slower: 2.09 -> 2.37 ms per POMO episode)
   template <int OPT, bool COMPACT = true>
@@ -514,9 +527,7 @@ struct GreedyRow {
     float m = NEG_INF;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
-      float t = v[k];
-      if (OPT & kOptClip) t = (kCompact ? t : clip_tanh<OPT>(t)) * clip;
-      if (OPT & kOptTemp) t = t / temp;
+      float t = kCompact ? z_scale<OPT>(v[k], clip, temp) : z_of<OPT>(v[k], clip, temp);
       t = allowed(k) ? t : NEG_INF;
       v[k] = t;
       m = fmaxf(m, t);
@@ -544,18 +555,24 @@ struct GreedyRow {
   // only needs whether any lane of the wave failed, one ballot): the lane is certified
   // when each of its elements other than sel trails by more than delta (masked entries
   // are -inf; a NaN fails the comparison).
+  // the L part of the bound: 2 x (2 ulp) of |L| + 1, margin included
+  static __device__ __forceinline__ float delta_l(float L) {
+    int e;
+    frexpf(fabsf(L) + 1.f, &e);  // |L| + 1 < 2^e: ulp(L) <= 2^(e - 24)
+    return ldexpf(1.f, e - 22) + 1e-7f;
+  }
+  template <int OPT>
+  static __device__ __forceinline__ float delta_z(float clip, float temp) {
+    if (!(OPT & kOptClip)) return 0.f;
+    int ec;
+    frexpf(clip, &ec);
+    const float ez = clip * 1.5e-6f + ldexpf(3.f, ec - 24);
+    return 2.f * ((OPT & kOptTemp) ? ez / temp : ez);
+  }
   template <int OPT>
   __device__ __forceinline__ bool certify(float L, int sel, int c0, int N, float clip,
                                           float temp) const {
-    int e;
-    frexpf(fabsf(L) + 1.f, &e);               // |L| + 1 < 2^e: ulp(L) <= 2^(e - 24)
-    float delta = ldexpf(1.f, e - 22) + 1e-7f;  // 2 x (2 ulp), margin included
-    if (OPT & kOptClip) {
-      int ec;
-      frexpf(clip, &ec);
-      const float ez = clip * 1.5e-6f + ldexpf(3.f, ec - 24);
-      delta += 2.f * ((OPT & kOptTemp) ? ez / temp : ez);
-    }
+    const float delta = delta_l(L) + delta_z<OPT>(clip, temp);
     // the lane's runner-up: the largest v[k] other than sel's (masked and past-the-row slots
     // are -inf; a NaN anywhere makes L NaN, which fails the finiteness test).  One max chain
     // instead of a per-slot test (r04: certified kernel 20.3 -> 18.4 us at 102,400 x 100)
@@ -577,10 +594,13 @@ struct GreedyRow {
 };
 
 // One row's greedy step on the GreedyRow engine: softmax_shift + select, or, with
-// kOptCert, the fast math certified per row and the exact math for any wave that holds an
-// uncertified valid row (wave-uniform branch: the group reductions need every lane).
-// Returns the action; L and lp as select().  The fallback recomputes into g itself (the
-// caller may read g.v afterwards: the full log-probabilities).  Measured and dropped (r04):
+// kOptCert, the fast math certified per row and, for any wave that holds an uncertified
+// valid row (wave-uniform branch: the group reductions need every lane), the exact z of
+// the row's candidates (tier 1) or the exact math for the whole wave (tier 2).  Returns
+// the action; L and lp as select().  g.v afterwards: the fast shifted values, or after
+// tier 2 the exact ones (the full log-probabilities, either within the certified
+// tolerance).  r04: the old fallback (the exact row reloaded from HBM for the whole wave)
+// cost 2.5 us of tail on a 19 us launch for 15 of 25,600 waves.  Measured and dropped (r04):
 // the fallback as a called (noinline) function -- the callee's registers count toward the
 // kernel's, 72 VGPRs; a waves-per-EU floor of 8 -- spills, 22.6-24.4 us; the compacted
 // tanh in the fallback -- 79 VGPRs.
@@ -590,6 +610,12 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
                                           float& lp, const float* lrow, const uint8_t* mrow) {
   if constexpr ((OPT & kOptCert) != 0) {
     constexpr int OF = (OPT & ~kOptCert) | kOptFast, OE = OPT & ~(kOptCert | kOptFast);
+    using GR = GreedyRow<RL, EPL, VW>;
+    // the raw logits stashed in the group's LDS row (lane sl: slots sl*EPL ..): the
+    // fallbacks read them there instead of from HBM (the fast math does not use the row)
+    float* stash = lds_row + sl * EPL;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) stash[k] = g.v[k];
     L = g.template softmax_shift<OF>(clip, temp, N, sl, lds_row);
     int sel = g.select(L, c0, lp);
     const bool ok = !valid || g.template certify<OF>(L, sel, c0, N, clip, temp);
@@ -598,18 +624,61 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
 #elif defined(CO_DIAG_CERT_NEVER)
     if (__any(!ok) && N < 0) {
 #else
-    if (__any(!ok)) {  // rare: the exact evaluation for the whole wave
+    if (__any(!ok)) {  // rare (15 of 25,600 waves at the POMO timing shape)
 #endif
-
-      // the raw row is read again (an L2 hit) rather than kept in EPL registers through
-      // the fast path: the kernel's VGPR count is the fast path's
-      g.load(valid, N, lrow, mrow, c0);
-      L = g.template softmax_shift<OE, false>(clip, temp, N, sl, lds_row);
-      sel = g.select(L, c0, lp);
-#ifdef CO_DIAG_CERT_COUNT  // diagnostic only: marks the rows of waves that fell back
-      lp = -12345.f;
+      // the stash is re-read from LDS (a compiler barrier: forwarding the stored registers
+      // instead would keep EPL more VGPRs live through the fast path)
+      asm volatile("" ::: "memory");
+      const int grp = lane_id() / RL;
+      const uint64_t gmask = (RL == 64 ? ~0ull : ((1ull << RL) - 1ull)) << (grp * RL);
+      const bool row_ok = (__ballot(!ok) & gmask) == 0ull;
+      // Tier 1: the exact processed logit z of the candidates only -- the elements the
+      // bound did not rule out (v[k] >= -delta): the exact maximum is one of them.  The
+      // action is the first index of the exact maximum unless a candidate before it could
+      // round to the same log-probability (|z_k - m| within the L part of the bound); then,
+      // and for rows whose L is not finite, tier 2.  The row keeps the fast log-sum-exp:
+      // logp = the fast v of the exact action - L (the certified rows' accuracy).
+      const float dz = GR::template delta_z<OF>(clip, temp), dl = GR::delta_l(L);
+      uint32_t pend = 0u;
+#pragma unroll
+      for (int k = 0; k < EPL; ++k)
+        if (valid && !row_ok && g.v[k] >= -(dl + dz)) pend |= 1u << k;
+      // one exact z per lane (one tanh code copy; the candidates are usually the top two
+      // and in different lanes): a lane with two or more sends the row to tier 2
+      const int kc = pend ? __builtin_ctz(pend) : 0;
+      const float zc = pend ? GR::template z_of<OE>(stash[kc], clip, temp) : -__builtin_inff();
+      const bool multi = (pend & (pend - 1u)) != 0u;
+      const float mz = grp_max<RL>(zc);
+      const int wi = grp_min_int<RL>(pend && zc == mz ? c0 + kc : 0x7fffffff);
+      const bool amb = (__ballot(multi || (pend && c0 + kc < wi && zc - mz >= -dl)) & gmask) !=
+                       0ull;  // group-uniform from here on
+      const bool fix = valid && !row_ok;
+      const bool tier2 = fix && (amb || !__builtin_isfinite(L) || wi == 0x7fffffff);
+      float lw = -__builtin_inff();
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) lw = c0 + k == wi ? g.v[k] - L : lw;
+      lw = grp_max<RL>(lw);  // every lane joins the group reduction
+      if (fix && !tier2) {
+        lp = lw;
+        sel = wi;
+#ifdef CO_DIAG_CERT_COUNT  // diagnostic only: marks the rows resolved by tier 1
+        lp = -23456.f;
 #endif
+      }
+      // Tier 2 (rarer still): the whole wave in the exact math from the stash (for the
+      // other rows the same action, their exact logp)
+      if (__any(tier2)) {
+#pragma unroll
+        for (int k = 0; k < EPL; ++k) g.v[k] = stash[k];
+        L = g.template softmax_shift<OE, false>(clip, temp, N, sl, lds_row);
+        sel = g.select(L, c0, lp);
+#ifdef CO_DIAG_CERT_COUNT  // diagnostic only: marks the rows of tier 2
+        if (tier2) lp = -12345.f;
+#endif
+      }
     }
+    (void)lrow;
+    (void)mrow;
     return sel;
   } else {
     L = g.template softmax_shift<OPT>(clip, temp, N, sl, lds_row);

@@ -639,8 +639,17 @@ __host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O
 #define CO_SLAP_LATE 0  // 1: the coordinates, 2: also the picklist loaded after the step loop
 #endif
 
+#ifndef CO_SLAP_WPE
+#define CO_SLAP_WPE 0  // > 0: amdgpu_waves_per_eu floor (SGPRs cap the kernel at 7 waves)
+#endif
+#if CO_SLAP_WPE > 0
+#define CO_SLAP_ATTR __attribute__((amdgpu_waves_per_eu(CO_SLAP_WPE)))
+#else
+#define CO_SLAP_ATTR
+#endif
+
 template <int G, int EPL, bool CLOSEST>
-__global__ __launch_bounds__(256) void slap_group_kernel(
+__global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     int64_t B, int L, int P, int O, int K, const float2* __restrict__ locs,
     const int64_t* __restrict__ picklist, const float* __restrict__ depot_dist,
     const int32_t* __restrict__ assign_in, const int64_t* __restrict__ acts_in,

@@ -86,6 +86,9 @@ __global__ __launch_bounds__(256) void tsp_step_kernel(int64_t B, int N, const i
 #define CO_TSP_SCUT 0  // timing diagnostic only: 1 no row epilogue, 2 no mask store
 #endif
 
+#ifndef CO_TSP_NT
+#define CO_TSP_NT 0  // variants: 1 mask words, 2 row scalars stored, 4 mask words loaded non-temporal
+#endif
 #ifndef CO_TSP_UNR
 #define CO_TSP_UNR 1  // row groups per wave (all their loads issued before the first use)
 #endif
@@ -136,7 +139,9 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
       const int c = CO_TSP_WORD(k);
-      w[u][k] = (valid[u] && c < W) ? src[c] : 0u;
+      w[u][k] = (valid[u] && c < W)
+                    ? ((CO_TSP_NT & 4) ? __builtin_nontemporal_load(src + c) : src[c])
+                    : 0u;
     }
   }
 #pragma unroll
@@ -162,14 +167,20 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
       const int c = CO_TSP_WORD(k);
-      if (valid[u] && c < W && !(CO_TSP_SCUT & 2)) dst[c] = w[u][k];
+      if (valid[u] && c < W && !(CO_TSP_SCUT & 2)) {
+        if (CO_TSP_NT & 1) __builtin_nontemporal_store(w[u][k], dst + c);
+        else dst[c] = w[u][k];
+      }
     }
     const bool any_left = (__ballot(left != 0) & gmask) != 0;
     if constexpr (G >= 8) {
       if (valid[u] && !(CO_TSP_SCUT & 1)) {
         int64_t* d8 = sl == 0 ? epi.i_out : sl == 1 ? epi.first_out : epi.cur_out;
         const int64_t v8 = sl == 0 ? rs[u] + 1 : (sl == 1 && !epi.take_first) ? rs[u] : a_raw[u];
-        if (sl < 3 && d8) d8[r] = v8;
+        if (sl < 3 && d8) {
+          if (CO_TSP_NT & 2) __builtin_nontemporal_store(v8, d8 + r);
+          else d8[r] = v8;
+        }
         if (sl == 3 || sl == 4) (sl == 3 ? epi.done : epi.reward)[r] = sl == 3 ? !any_left : 0;
       }
     } else if (valid[u] && sl == 0 && !(CO_TSP_SCUT & 1)) {

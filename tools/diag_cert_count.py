@@ -1,6 +1,6 @@
 """Diagnostic: how many waves of the certified greedy TSP decode step take the exact
 fallback at the POMO timing shape (tools/run_mode.py decode_kernels inputs), with a
-library built with -DCO_DIAG_CERT_COUNT (the fallback marks its rows' logp -12345)."""
+library built with -DCO_DIAG_CERT_COUNT (tier-1 rows' logp -23456, tier-2 rows' -12345)."""
 import os
 import sys
 
@@ -34,6 +34,7 @@ for seed, clip in ((3, 10.0), (3, 0.0), (4, 10.0)):
                       outs[4].data_ptr(), 0, outs[5].data_ptr(), outs[6].data_ptr(), None,
                       st.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    rows = int((outs[1] == -12345.0).sum())
-    print(f"seed {seed} clip {clip}: {rows} rows in fallback waves (4 rows a wave: {rows / 4:.0f} "
-          f"of {b // 4} waves)")
+    t1 = int((outs[1] == -23456.0).sum())
+    t2 = int((outs[1] == -12345.0).sum())
+    print(f"seed {seed} clip {clip}: {t1} rows resolved by tier 1 (exact z of the candidates), "
+          f"{t2} rows in tier-2 waves (the exact row), of {b} rows")

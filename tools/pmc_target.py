@@ -17,7 +17,46 @@ from rl4co_slap_amd import _native  # noqa: E402
 from rl4co_slap_amd.rollout import engine  # noqa: E402
 
 _native.load()
-if args.kernel.startswith("tsp"):
+
+
+class _Loop:
+    """A drop-in decode loop (ConstructivePolicy + env, stub decoder, certified greedy) as
+    an object with run_eager(), for the fused decode + env step kernels' counters."""
+
+    def __init__(self, env, td, logits, name):
+        from rl4co_slap_amd.rollout.constructive import ConstructivePolicy, LogitsDecoder
+        from rl4co_slap_amd.td import TensorDict
+
+        self.env, self.td, self.TD = env, td, TensorDict
+        self.pol = ConstructivePolicy(None, LogitsDecoder(lambda t: logits), env_name=name,
+                                      tanh_clipping=10.0)
+
+    def run_eager(self):
+        b = next(iter(self.td.values())).shape[0]
+        t = self.env.reset(self.TD(dict(self.td), [b]))
+        self.pol(t, self.env, phase="test", decode_type="greedy")
+
+
+if args.kernel == "dropin_cvrp":
+    from rl4co_slap_amd.envs import CVRPEnv
+
+    torch.manual_seed(1234)
+    la = torch.rand(32768, 101, 2)
+    td = {"depot": la[:, 0].contiguous().to(dev), "locs": la[:, 1:].contiguous().to(dev),
+          "demand": (((torch.rand(32768, 100) * 9).int() + 1).float() / 50.0).to(dev)}
+    ep = _Loop(CVRPEnv(generator_params=dict(num_loc=100), device=dev), td,
+               torch.randn(32768, 101).to(dev), "cvrp")
+elif args.kernel == "dropin_slap":
+    import numpy as np
+
+    from rl4co_slap_amd.envs import SLAPEnv
+    from rl4co_slap_amd.envs.slap import SLAPGenerator
+
+    torch.manual_seed(1234)
+    np.random.seed(1234)
+    td = dict(SLAPGenerator(materialize_dist_mat=False)(65536).to(dev).items())
+    ep = _Loop(SLAPEnv(device=dev), td, torch.randn(65536, 100).to(dev), "slap")
+elif args.kernel.startswith("tsp"):
     torch.manual_seed(1234)
     locs = torch.rand(65536, 100, 2)
     torch.manual_seed(4321)
