@@ -165,6 +165,17 @@ __device__ __forceinline__ float grp_max(float v) {
     return __float_as_uint(fmaxf(__uint_as_float(x), __uint_as_float(y)));
   }));
 }
+// max over the group on order-preserving ints (one DPP max per stage; the float max needs
+// a canonicalising move per stage).  A NaN member may win (the callers' sums go NaN anyway)
+template <int RL>
+__device__ __forceinline__ float grp_max_ord(float v) {
+  const int b = __float_as_int(v);
+  int o = b ^ ((b >> 31) & 0x7fffffff);
+  o = (int)grp_reduce<RL>((uint32_t)o, [](uint32_t x, uint32_t y) {
+    return (uint32_t)max((int)x, (int)y);
+  });
+  return __int_as_float(o ^ ((o >> 31) & 0x7fffffff));
+}
 template <int RL>
 __device__ __forceinline__ float grp_sum(float v) {
   return __uint_as_float(grp_reduce<RL>(__float_as_uint(v), [](uint32_t x, uint32_t y) {

@@ -52,6 +52,10 @@ __device__ __forceinline__ float co_exp_fast(float x) { return co_exp2(x * 1.442
 // (GreedyRow kernels only, CO_DECODE_CERTIFIED: fast math, then the exact recomputation
 // for every wave holding a row whose fast argmax the error bound cannot certify)
 constexpr int kOptClip = 1, kOptTemp = 2, kOptFast = 4, kOptCert = 8;
+// kOptLean (internal: the certified path's fast pass in GreedyRow): the padded slots hold
+// -inf already (no per-slot row-bound select in the exp sum), the log on v_log_f32, the
+// group max on ordered ints, the lane's top two kept for the certification
+constexpr int kOptLean = 16;
 #ifndef CO_TANH_COMPACT
 #define CO_TANH_COMPACT 1  // GreedyRow: exact tanh of allowed elements only, wave-compacted
 #endif
@@ -80,6 +84,13 @@ __device__ __forceinline__ float row_log_sum_exp(const float (&d)[EPL], int N, i
   if (OPT & kOptFast) {
 #endif
     float s = 0.f;
+    if constexpr ((OPT & kOptLean) != 0) {
+      // every slot past N is -inf (masked) here: e^-inf = 0 needs no row-bound select;
+      // the sum is >= 1 (the maximum's term), so v_log_f32 needs no denormal scaling
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) s += co_exp_fast(d[k]);
+      return __builtin_amdgcn_logf(grp_sum<RL>(s)) * 0.69314718055994531f;
+    }
 #pragma unroll
     for (int k = 0; k < EPL; ++k) s += c0 + k < N ? co_exp_fast(d[k]) : 0.f;
     return logf(grp_sum<RL>(s));
@@ -421,6 +432,7 @@ struct GreedyRow {
   static_assert(EPL % 4 == 0, "GreedyRow keeps the mask in u32 words");
   float v[EPL];
   uint32_t mw[EPL / 4];
+  float top1 = 0.f, top2 = 0.f;  // kOptLean: the lane's largest two shifted values
 
   __device__ __forceinline__ void load(bool valid, int N, const float* lrow, const uint8_t* mrow,
                                        int c0) {
@@ -524,15 +536,28 @@ struct GreedyRow {
     // exact tanh clipping: tanh of the allowed elements, wave-compacted (above)
     constexpr bool kCompact = COMPACT && (OPT & kOptClip) && !(OPT & kOptFast) && CO_TANH_COMPACT;
     if constexpr (kCompact) tanh_allowed_compact(lds_row - (lane_id() / RL) * (RL * EPL));
-    float m = NEG_INF;
+    float m = NEG_INF, m2 = NEG_INF;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
       float t = kCompact ? z_scale<OPT>(v[k], clip, temp) : z_of<OPT>(v[k], clip, temp);
       t = allowed(k) ? t : NEG_INF;
       v[k] = t;
-      m = fmaxf(m, t);
+      if constexpr ((OPT & kOptLean) != 0) {
+        m2 = __builtin_amdgcn_fmed3f(m, m2, t);  // the lane's second largest (m2 <= m)
+        m = __builtin_fmaxf(m, t);
+      } else {
+        m = fmaxf(m, t);
+      }
     }
-    m = grp_max<RL>(m);
+    if constexpr ((OPT & kOptLean) != 0) {
+      // NaN anywhere makes L NaN below whichever member the max returns
+      const float lm = m;
+      m = grp_max_ord<RL>(m);
+      top1 = lm - m;
+      top2 = m2 - m;
+    } else {
+      m = grp_max<RL>(m);
+    }
 #pragma unroll
     for (int k = 0; k < EPL; ++k) v[k] = v[k] - m;
     return row_log_sum_exp<RL, EPL, OPT>(v, N, sl, lds_row);
@@ -573,6 +598,13 @@ struct GreedyRow {
   __device__ __forceinline__ bool certify(float L, int sel, int c0, int N, float clip,
                                           float temp) const {
     const float delta = delta_l(L) + delta_z<OPT>(clip, temp);
+    if constexpr ((OPT & kOptLean) != 0) {
+      // the lane's runner-up from its top two: the second if the lane holds sel (a tie
+      // with sel in the same lane leaves top2 = 0), else its largest (a tie in another
+      // lane: 0)
+      const float r = (unsigned)(sel - c0) < (unsigned)EPL ? top2 : top1;
+      return __builtin_isfinite(L) && r < -delta;
+    }
     // the lane's runner-up: the largest v[k] other than sel's (masked and past-the-row slots
     // are -inf; a NaN anywhere makes L NaN, which fails the finiteness test).  One max chain
     // instead of a per-slot test (r04: certified kernel 20.3 -> 18.4 us at 102,400 x 100)
@@ -582,12 +614,16 @@ struct GreedyRow {
     return __builtin_isfinite(L) && r < -delta;
   }
 
-  // greedy action of the row (valid on every lane of the group) and its logp
+  // greedy action of the row (valid on every lane of the group) and its logp.  LEAN (the
+  // certified fast pass): the first index of the maximum itself (v = 0) -- a rounding tie
+  // with it (fl(v - L) == fl(-L) for some v < 0) fails the certification anyway
+  template <bool LEAN = false>
   __device__ __forceinline__ int select(float L, int c0, float& lp) const {
     lp = 0.f - L;
     int idx = 0x7fffffff;
 #pragma unroll
-    for (int k = EPL - 1; k >= 0; --k) idx = (v[k] - L == lp) ? c0 + k : idx;
+    for (int k = EPL - 1; k >= 0; --k)
+      idx = (LEAN ? v[k] == 0.f : v[k] - L == lp) ? c0 + k : idx;
     idx = grp_min_int<RL>(idx);
     return idx == 0x7fffffff ? 0 : idx;  // no match only when L is NaN: all logp NaN
   }
@@ -609,7 +645,8 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
                                           float temp, int sl, int c0, float* lds_row, float& L,
                                           float& lp, const float* lrow, const uint8_t* mrow) {
   if constexpr ((OPT & kOptCert) != 0) {
-    constexpr int OF = (OPT & ~kOptCert) | kOptFast, OE = OPT & ~(kOptCert | kOptFast);
+    constexpr int OF = (OPT & ~kOptCert) | kOptFast | kOptLean,
+                  OE = OPT & ~(kOptCert | kOptFast);
     using GR = GreedyRow<RL, EPL, VW>;
     // the raw logits stashed in the group's LDS row (lane sl: slots sl*EPL ..): the
     // fallbacks read them there instead of from HBM (the fast math does not use the row)
@@ -617,7 +654,7 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
 #pragma unroll
     for (int k = 0; k < EPL; ++k) stash[k] = g.v[k];
     L = g.template softmax_shift<OF>(clip, temp, N, sl, lds_row);
-    int sel = g.select(L, c0, lp);
+    int sel = g.template select<true>(L, c0, lp);
     const bool ok = !valid || g.template certify<OF>(L, sel, c0, N, clip, temp);
 #if defined(CO_DIAG_CERT_NOFALLBACK)  // timing diagnostics only: no fallback code at all /
     if (false) {                          // the fallback compiled in but never taken

@@ -60,9 +60,14 @@ def _decode(x, mask, clip, temp, mode):
     return act, lp
 
 
-@pytest.mark.parametrize("n", [20, 100, 150])
+@pytest.mark.parametrize("n", [20, 100, 150, 600, 1500])
 @pytest.mark.parametrize("clip,temp", [(10.0, 1.0), (0.0, 1.0), (10.0, 0.5), (0.0, 2.0)])
 def test_certified_greedy_actions_equal_exact(dev, n, clip, temp):
+    """Adversarial rows through both fallback tiers: near-ties before and after the pick
+    (tier 1 resolves them from the exact z of the candidates; a candidate before the pick
+    within the rounding bound, or two candidates in one lane, takes tier 2), exact ties,
+    saturated ties, NaN / inf / all-masked rows (tier 2); N up to 1,500 (16 / 32 elements
+    per lane)."""
     x, mask = _adversarial_logits(4096, n, 3 + n, dev)
     a_e, lp_e = _decode(x, mask, clip, temp, 0)
     a_c, lp_c = _decode(x, mask, clip, temp, nat.DECODE_CERTIFIED)
