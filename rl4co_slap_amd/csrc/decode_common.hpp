@@ -657,11 +657,17 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
     int sel = g.template select<true>(L, c0, lp);
     const bool ok = !valid || g.template certify<OF>(L, sel, c0, N, clip, temp);
 #if defined(CO_DIAG_CERT_NOFALLBACK)  // timing diagnostics only: no fallback code at all /
-    if (false) {                          // the fallback compiled in but never taken
-#elif defined(CO_DIAG_CERT_NEVER)
+    if (false) {                          // the fallback compiled in but never taken /
+#elif defined(CO_DIAG_CERT_NEVER)         // the certification's cost alone
     if (__any(!ok) && N < 0) {
+#elif defined(CO_DIAG_CERT_TRIVIAL)
+    if (__any(!ok) && N < 0) {
+      lp += 1.f;
+    }
+    if (false) {
 #else
-    if (__any(!ok)) {  // rare (15 of 25,600 waves at the POMO timing shape)
+    // rare (15 of 25,600 waves at the POMO timing shape): laid out after the hot path
+    if (__builtin_expect(__any(!ok), 0)) {
 #endif
       // the stash is re-read from LDS (a compiler barrier: forwarding the stored registers
       // instead would keep EPL more VGPRs live through the fast path)
@@ -704,7 +710,11 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
       }
       // Tier 2 (rarer still): the whole wave in the exact math from the stash (for the
       // other rows the same action, their exact logp)
+#ifdef CO_DIAG_T2_NEVER  // timing diagnostic only: tier 2 compiled in but never taken
+      if (__any(tier2) && N < 0) {
+#else
       if (__any(tier2)) {
+#endif
 #pragma unroll
         for (int k = 0; k < EPL; ++k) g.v[k] = stash[k];
         L = g.template softmax_shift<OE, false>(clip, temp, N, sl, lds_row);
