@@ -632,7 +632,8 @@ struct GreedyRow {
 // One row's greedy step on the GreedyRow engine: softmax_shift + select, or, with
 // kOptCert, the fast math certified per row and, for any wave that holds an uncertified
 // valid row (wave-uniform branch: the group reductions need every lane), the exact z of
-// the row's candidates (tier 1) or the exact math for the whole wave (tier 2).  Returns
+// the row's candidates (tier 1) or the exact math for the whole wave (tier 2), both from
+// the raw logits read again.  Returns
 // the action; L and lp as select().  g.v afterwards: the fast shifted values, or after
 // tier 2 the exact ones (the full log-probabilities, either within the certified
 // tolerance).  r04: the old fallback (the exact row reloaded from HBM for the whole wave)
@@ -640,6 +641,10 @@ struct GreedyRow {
 // the fallback as a called (noinline) function -- the callee's registers count toward the
 // kernel's, 72 VGPRs; a waves-per-EU floor of 8 -- spills, 22.6-24.4 us; the compacted
 // tanh in the fallback -- 79 VGPRs.
+#ifndef CO_CERT_STASH
+#define CO_CERT_STASH 0  // 1: the certified fallbacks read the raw logits from an LDS stash (r04: +1.8 us)
+#endif
+
 template <int OPT, int RL, int EPL, int VW>
 __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid, int N, float clip,
                                           float temp, int sl, int c0, float* lds_row, float& L,
@@ -648,11 +653,16 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
     constexpr int OF = (OPT & ~kOptCert) | kOptFast | kOptLean,
                   OE = OPT & ~(kOptCert | kOptFast);
     using GR = GreedyRow<RL, EPL, VW>;
-    // the raw logits stashed in the group's LDS row (lane sl: slots sl*EPL ..): the
-    // fallbacks read them there instead of from HBM (the fast math does not use the row)
+    // the raw logits for the fallbacks: read again from the row (an L2 / HBM read, only in
+    // the rare fallback waves).  Stashing them in the group's LDS row instead (2
+    // ds_write_b128 per lane on the hot path) measured +1.8 us on a 14.8 us launch (r04).
+#if !CO_CERT_STASH  // the fallbacks read the raw row again (an L2 / HBM read)
+    const float* stash = lrow + c0;
+#else
     float* stash = lds_row + sl * EPL;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) stash[k] = g.v[k];
+#endif
     L = g.template softmax_shift<OF>(clip, temp, N, sl, lds_row);
     int sel = g.template select<true>(L, c0, lp);
     const bool ok = !valid || g.template certify<OF>(L, sel, c0, N, clip, temp);
@@ -663,6 +673,12 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
 #elif defined(CO_DIAG_CERT_TRIVIAL)
     if (__any(!ok) && N < 0) {
       lp += 1.f;
+    }
+    if (false) {
+#elif defined(CO_DIAG_CERT_STASHONLY)  // the certification and the stash, no fallback code
+    if (__any(!ok) && N < 0) {
+      asm volatile("" ::: "memory");
+      lp += stash[0];
     }
     if (false) {
 #else
@@ -715,8 +731,12 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
 #else
       if (__any(tier2)) {
 #endif
+#if !CO_CERT_STASH
+        g.load(valid, N, lrow, mrow, c0);
+#else
 #pragma unroll
         for (int k = 0; k < EPL; ++k) g.v[k] = stash[k];
+#endif
         L = g.template softmax_shift<OE, false>(clip, temp, N, sl, lds_row);
         sel = g.select(L, c0, lp);
 #ifdef CO_DIAG_CERT_COUNT  // diagnostic only: marks the rows of tier 2
