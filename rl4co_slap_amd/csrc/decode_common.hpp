@@ -438,34 +438,6 @@ struct GreedyRow {
                                        int c0) {
     using F = typename Chunk<VW>::F;
     using M = typename Chunk<VW>::M;
-    if constexpr (VW == 3) {
-      if (N >= 4) {
-        // branch-free: every lane loads one 4-element chunk at cs = min(c, N - 4) (dword-
-        // aligned logits, byte-aligned mask word) and shifts it by c - cs; chunks past the
-        // row read the last chunk and mask it all.  (A lane-divergent partial-chunk path
-        // made the compiler wait for every outstanding load -- the fused env steps' LDS-DMA
-        // staging included -- before the next chunk's load: r04.)
-#pragma unroll
-        for (int j = 0; j < EPL / 4; ++j) {
-          const int c = c0 + 4 * j;
-          const int cs = c < N - 4 ? c : N - 4;
-          const int sh = c - cs;  // 0 inside the row, 1..3 on its partial last chunk, >= 4 past it
-          const F x = *reinterpret_cast<const F*>(lrow + cs);
-          const uint32_t mraw = mrow ? (uint32_t) * reinterpret_cast<const M*>(mrow + cs) : 0x01010101u;
-          const int nin = N - c;  // elements of this chunk inside the row
-          const uint32_t keep = !valid || nin <= 0 ? 0u : nin >= 4 ? 0xffffffffu : (1u << (8 * nin)) - 1u;
-          mw[j] = (sh >= 4 ? 0u : (mraw >> (8 * sh))) & keep;
-          // element q of the chunk is x[q + sh] (sh <= 3; past the row the values are masked)
-          const bool s1 = sh == 1, s2 = sh == 2, s3 = sh == 3;
-          const float x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
-          v[4 * j + 0] = s3 ? x3 : s2 ? x2 : s1 ? x1 : x0;
-          v[4 * j + 1] = s2 ? x3 : s1 ? x2 : x1;
-          v[4 * j + 2] = s1 ? x3 : x2;
-          v[4 * j + 3] = x3;
-        }
-        return;
-      }
-    }
 #pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {
       const int c = c0 + 4 * j;

@@ -297,17 +297,11 @@ struct CvrpStage {
       const uint32_t cust = c == 0 ? own & ~0xffu : own;  // the depot column excluded
       uint32_t x = 0u;
       float d[4];
-      // every LDS read unconditional (indices clamped into the staged row, values outside
-      // the row selected away): no exec-masked branch around each read
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool in = q < nown;
-        const int cv = c + q < NC - 1 ? c + q : NC - 1;
-        const int cd = c + q - 1 < 0 ? 0 : (c + q - 1 > Nn - 1 ? Nn - 1 : c + q - 1);
-        const uint32_t b = vb_s[cv];
-        const float dv = dm_s[cd];
-        x |= in ? b << (8 * q) : 0u;
-        d[q] = (in && c + q >= 1) ? dv : 0.f;
+        x |= in ? (uint32_t)vb_s[c + q] << (8 * q) : 0u;
+        d[q] = (in && c + q >= 1) ? dm_s[c + q - 1] : 0.f;
       }
       const int ea = a - c;  // the action's byte, if in this chunk: scatter(..., 1)
       if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
