@@ -361,3 +361,71 @@ def test_native_step_glue_equals_python_fused_path(dev, monkeypatch, name, decod
         assert torch.equal(a[k], b_[k]), k
     for k in keys:
         assert torch.equal(sa[k], sb[k]), k
+
+
+@pytest.mark.parametrize("env_name", ["cvrp", "slap"])
+def test_fused_env_decode_certified_actions_equal_exact_on_near_ties(dev, env_name):
+    """The fused decode + env steps in the certified math (the drop-in default) pick the
+    exact path's greedy action on adversarial rows -- near-ties straddling the
+    certification margin before and after the pick (the fallback's tier 1), ties in one
+    lane, exact / saturated ties, NaN / inf / all-masked rows (tier 2) -- with logp within
+    1e-5 of the exact one; the env state follows the action."""
+    from test_gpu_decode_certified import _adversarial_logits
+
+    from rl4co_slap_amd import _native as nat
+
+    g = torch.Generator().manual_seed(23)
+    b = 2048
+    n = 100 if env_name == "slap" else 100  # SLAP: L locations; CVRP: N customers (N+1 columns)
+    nc = n if env_name == "slap" else n + 1
+    x, m = _adversarial_logits(b, nc, 41, dev)
+    if env_name == "cvrp":
+        m[:, 0] = True  # a feasible depot keeps every row's mask a reachable CVRP mask
+    for clip in (10.0, 0.0):
+        # the exact reference action / logp (co_decode_step, no math flag)
+        act_e = torch.empty(b, dtype=torch.int64, device=dev)
+        lp_e = torch.empty(b, dtype=torch.float32, device=dev)
+        st = torch.zeros(1, dtype=torch.int32, device=dev)
+        nat.call("co_decode_step", b, nc, nat.ptr(x), nc, nat.ptr(m), clip, 1.0, 0, None,
+                 nat.ptr(act_e), nat.ptr(lp_e), None, 0, 0, nat.ptr(st), nat.stream_of(x))
+        act = torch.empty(b, dtype=torch.int64, device=dev)
+        lp = torch.empty(b, dtype=torch.float32, device=dev)
+        st = torch.zeros(1, dtype=torch.int32, device=dev)
+        if env_name == "cvrp":
+            demand = (torch.randint(1, 10, (b, n), generator=g).float() / 30.0).to(dev)
+            used = torch.zeros(b, 1, device=dev)
+            vcap = torch.ones(b, 1, device=dev)
+            vis = (~m).to(torch.uint8)
+            vis[:, 0] = 1
+            outs = [torch.empty_like(used), torch.empty_like(vis),
+                    torch.empty(b, 1, dtype=torch.int64, device=dev),
+                    torch.empty(b, dtype=torch.bool, device=dev),
+                    torch.empty(b, dtype=torch.bool, device=dev), torch.empty_like(m)]
+            nat.call("co_cvrp_decode_step", b, n, nat.ptr(x), nc, nat.ptr(m), clip, 1.0,
+                     nat.DECODE_CERTIFIED, None, nat.ptr(act), nat.ptr(lp), 0, 0, nat.ptr(demand),
+                     nat.ptr(used), nat.ptr(outs[0]), nat.ptr(vcap), nat.ptr(vis),
+                     nat.ptr(outs[1]), nat.ptr(outs[2]), nat.ptr(outs[3]), nat.ptr(outs[4]),
+                     nat.ptr(outs[5]), None, nat.ptr(st), nat.stream_of(x))
+            rows = torch.arange(b, device=dev)
+            ok = act < nc
+            assert bool((outs[1][rows[ok], act[ok]] == 1).all())  # the action's node visited
+        else:
+            p = 20
+            tc = torch.rand(b, p, generator=g).to(dev)
+            asg_in = torch.full((b, p), -1, dtype=torch.int32, device=dev)
+            asg_out = torch.empty_like(asg_in)
+            i_in = torch.randint(0, p, (b, 1), generator=g).to(dev)
+            outs = [asg_out, torch.empty_like(m), torch.empty_like(i_in),
+                    torch.empty(b, 1, dtype=torch.bool, device=dev),
+                    torch.empty(b, 1, dtype=torch.bool, device=dev)]
+            nat.call("co_slap_decode_step", b, nc, p, nat.ptr(x), nc, nat.ptr(m), clip, 1.0,
+                     nat.DECODE_CERTIFIED, None, nat.ptr(act), nat.ptr(lp), 0, 0, nat.ptr(tc), p,
+                     nat.ptr(asg_in), nat.ptr(asg_out), nat.ptr(outs[1]), nat.ptr(i_in),
+                     nat.ptr(outs[2]), nat.ptr(outs[3]), nat.ptr(outs[4]), None, nat.ptr(st),
+                     nat.stream_of(x))
+            assert torch.equal(outs[2], i_in + 1)
+        torch.cuda.synchronize()
+        assert torch.equal(act, act_e), clip
+        fin = torch.isfinite(lp_e)
+        assert torch.equal(fin, torch.isfinite(lp))
+        assert bool(((lp - lp_e)[fin].abs() <= 1e-5 * lp_e[fin].abs().clamp(min=1)).all()), clip
