@@ -1,0 +1,7 @@
+# Round 4 last check on the final tree: the whole GPU suite and smoke().
+cd $GRAFT_REPO_ROOT
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
+  > gpurun_out/verify_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/verify_tests.log; echo "[$rc] gpu tests"
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error" gpurun_out/verify_tests.log | head -20; exit $rc; fi
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" 2>&1 | tail -2
