@@ -399,6 +399,42 @@ def cpu_baseline_cvrp(b=32768, n=100, episodes=5):
                       f"loop, median (min / max) of {episodes} episodes after 1 warm-up"}
 
 
+def cpu_baseline_pomo(b=256, n=100, episodes=5):
+    """The oracle's POMO TSP-100 episode (the restated multistart loop on
+    CPU, a stated subset of config 5's 8,192 x 100 envs): ``constructive_forward`` with
+    multistart greedy decoding (``decoding.py:265-313``: batchify x S, the start step,
+    N-1 decode steps of tanh clip 10 -> mask -> log_softmax -> argmax on fixed step-major
+    logits, as the GPU mode feeds them), the reward with its validity check, then the
+    shared-baseline REINFORCE loss (``pomo/model.py:87-144``, ``reinforce.py:97-115``).
+    B = 256 instances x S = 100 starts = 25,600 envs (the GPU mode: 1,024 x 100 per GPU)."""
+    from oracle.envs import TSPOracle
+    from oracle.rollout import constructive_forward, pomo_loss
+    from oracle.td import TD
+
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(1234)
+    locs = torch.rand(b, n, 2, generator=g)
+    logits = torch.randn(n - 1, n * b, n, generator=g)
+    env = TSPOracle(num_loc=n, seed=1234)
+    times = []
+    for _ in range(episodes + 1):
+        td = env.reset(TD({"locs": locs.clone()}, [b]))
+        it = iter(range(n - 1))
+        t0 = time.perf_counter()
+        out = constructive_forward(td, env, lambda t: logits[next(it)],
+                                   decode_type="multistart_greedy", tanh_clipping=10.0)
+        pomo_loss(out["reward"], out["log_likelihood"], n)
+        times.append(time.perf_counter() - t0)
+    return {**_spread(times, b * n * n), "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"oracle POMO TSP-{n} episode: constructive_forward multistart greedy "
+                      f"(batchify x {n} starts, start step + {n - 1} decode steps, tanh clip 10, "
+                      f"fixed step-major logits) + reward with validity + shared-baseline loss, "
+                      f"B={b} instances x {n} starts = {b * n} envs (config 5 subset; the GPU "
+                      f"mode runs 1,024 x {n} per GPU), median (min / max) of {episodes} "
+                      f"episodes after 1 warm-up"}
+
+
 def pmc_traffic(target, kernel_prefix):
     """HBM bytes per launch measured by rocprofv3 PMC passes (scripts/gpu_pmc.sh ->
     tools/pmc_summarize.py -> profiles/*_pmc_traffic.json, newest round first)."""
@@ -573,15 +609,20 @@ def main():
         if not args.no_modes:
             out["cpu_baseline_slap"] = cpu_baseline_slap()
             out["cpu_baseline_cvrp"] = cpu_baseline_cvrp()
+            out["cpu_baseline_pomo"] = cpu_baseline_pomo()
     if rank == 0:
         out["build"] = _native.provenance()  # the sources the measured library came from
         out["summary"] = summarize(out)
-        # contract keys first, then the short summary, the long mode tables last
+        # contract keys first, the long mode tables next, and the short records a reader
+        # (and the driver's stdout tail) needs LAST: the stepwise / SLAP-65,536 figures and
+        # the summary of every mode end the line
         order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
-                 "roofline", "cpu_baseline", "summary", "tsp_stepwise", "slap_b65536"]
+                 "roofline", "cpu_baseline"]
+        last = ["tsp_stepwise", "slap_b65536", "summary"]
         final = {key: out[key] for key in order if key in out}
-        final.update({key: v for key, v in out.items() if key not in final})
+        final.update({key: v for key, v in out.items() if key not in final and key not in last})
+        final.update({key: out[key] for key in last if key in out})
         print(json.dumps(final), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -624,7 +665,7 @@ def summarize(out):
     sk = out.get("step_kernels_vs_copy", {})
     if sk:
         sm["step_kernels_frac_of_copy"] = {k2: r(v["frac_of_copy"]) for k2, v in sk.items()}
-    for name in ("cpu_baseline", "cpu_baseline_slap", "cpu_baseline_cvrp"):
+    for name in ("cpu_baseline", "cpu_baseline_slap", "cpu_baseline_cvrp", "cpu_baseline_pomo"):
         c = out.get(name)
         if c:
             sm[name] = {"value": r(c["value"], 0), "min": r(c.get("value_min"), 0),

@@ -294,6 +294,18 @@ inline unsigned grid_for(int64_t work_items, int per_block, int64_t cap = 256 * 
   return (unsigned)g;
 }
 
+// A grid that covers the work exactly (kernels without a grid-stride loop: every row group
+// gets its wave), or 0 when it would exceed HIP's limit of 2^32 - 1 threads per grid
+// dimension -- the entry point then returns CO_E_INVAL instead of launching a grid that
+// skips rows.
+constexpr int64_t kMaxCoverThreads = ((int64_t)1 << 32) - 1;
+inline unsigned cover_grid(int64_t work_items, int per_block, int block_threads = 256) {
+  int64_t g = (work_items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g * (int64_t)block_threads > kMaxCoverThreads) return 0;
+  return (unsigned)g;
+}
+
 inline int launch_status() {
   hipError_t e = hipGetLastError();
   return e == hipSuccess ? CO_OK : (int)e;

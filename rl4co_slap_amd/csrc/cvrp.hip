@@ -1203,7 +1203,8 @@ extern "C" int co_cvrp_step(int64_t B, int64_t N, const int64_t* action, const f
     const int waves = not_done ? 16 : 4;
     const int64_t rows_per_wg = (int64_t)(64 / G) * Q * waves;
     const int64_t wgs = (B + rows_per_wg - 1) / rows_per_wg;
-    const unsigned grid = (unsigned)wgs;
+    const unsigned grid = cover_grid(wgs, 1, 64 * waves);
+    if (grid == 0) return CO_E_INVAL;
     hipStream_t s = (hipStream_t)stream;
 #define CO_CQ(K, W)                                                                         \
   hipLaunchKernelGGL((cvrp_step_rows_kernel<G, K, Q, W>), dim3(grid), dim3(64 * W), 0, s, B,  \
@@ -1226,7 +1227,8 @@ extern "C" int co_cvrp_step(int64_t B, int64_t N, const int64_t* action, const f
   int R = (int)((256 * kCvrpCpt * 16) / NC);
   R = (R > kCvrpMaxRows ? kCvrpMaxRows : R) & ~15;
   if (N >= 16 && aligned && R >= 16 && (size_t)R * N * sizeof(float) + 16 <= 64 * 1024) {
-    const unsigned grid = (unsigned)((B + R - 1) / R);
+    const unsigned grid = cover_grid(B, R);
+    if (grid == 0) return CO_E_INVAL;
     hipLaunchKernelGGL(cvrp_step_tile_kernel<256>, dim3(grid), dim3(256),
                        (size_t)R * N * sizeof(float) + 16, (hipStream_t)stream, B, (int)N, R, action,
                        demand, used_in, used_out, vcap, vis_in, vis_out, cur_out, done, reward,

@@ -11,6 +11,7 @@
 // Shared by decode_step.hip (co_decode_step[_ex], beam search) and decode_tsp.hip
 // (co_tsp_decode_step): two translation units, compiled in parallel.
 #include "co_common.hpp"
+#include "co_diag.hpp"
 #include "co_math.hpp"
 
 using namespace co;
@@ -65,10 +66,7 @@ constexpr int kOptLean = 16;
 
 template <int OPT>
 __device__ __forceinline__ float clip_tanh(float x) {
-#ifdef CO_DIAG_FASTTANH  // timing diagnostic: fast tanh inside the exact path
-  return co_tanh_fast(x);
-#endif
-  return (OPT & kOptFast) ? co_tanh_fast(x) : tanh_cr(x);
+  return ((OPT & kOptFast) || kDiagFastTanh) ? co_tanh_fast(x) : tanh_cr(x);
 }
 
 // exp-sum of a row (x already shifted by the row max; out-of-row slots excluded) and its
@@ -78,11 +76,7 @@ __device__ __forceinline__ float row_log_sum_exp(const float (&d)[EPL], int N, i
                                                  float* lds_row) {
   const int c0 = sl * EPL;
   float e[EPL];
-#ifdef CO_DIAG_FASTEXP  // timing diagnostic: fast exp-sum inside the exact path
-  if (true) {
-#else
-  if (OPT & kOptFast) {
-#endif
+  if ((OPT & kOptFast) || kDiagFastExp) {
     float s = 0.f;
     if constexpr ((OPT & kOptLean) != 0) {
       // every slot past N is -inf (masked) here: e^-inf = 0 needs no row-bound select;
@@ -641,9 +635,6 @@ struct GreedyRow {
 // the fallback as a called (noinline) function -- the callee's registers count toward the
 // kernel's, 72 VGPRs; a waves-per-EU floor of 8 -- spills, 22.6-24.4 us; the compacted
 // tanh in the fallback -- 79 VGPRs.
-#ifndef CO_CERT_STASH
-#define CO_CERT_STASH 0  // 1: the certified fallbacks read the raw logits from an LDS stash (r04: +1.8 us)
-#endif
 
 template <int OPT, int RL, int EPL, int VW>
 __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid, int N, float clip,
@@ -656,38 +647,12 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
     // the raw logits for the fallbacks: read again from the row (an L2 / HBM read, only in
     // the rare fallback waves).  Stashing them in the group's LDS row instead (2
     // ds_write_b128 per lane on the hot path) measured +1.8 us on a 14.8 us launch (r04).
-#if !CO_CERT_STASH  // the fallbacks read the raw row again (an L2 / HBM read)
     const float* stash = lrow + c0;
-#else
-    float* stash = lds_row + sl * EPL;
-#pragma unroll
-    for (int k = 0; k < EPL; ++k) stash[k] = g.v[k];
-#endif
     L = g.template softmax_shift<OF>(clip, temp, N, sl, lds_row);
     int sel = g.template select<true>(L, c0, lp);
     const bool ok = !valid || g.template certify<OF>(L, sel, c0, N, clip, temp);
-#if defined(CO_DIAG_CERT_NOFALLBACK)  // timing diagnostics only: no fallback code at all /
-    if (false) {                          // the fallback compiled in but never taken /
-#elif defined(CO_DIAG_CERT_NEVER)         // the certification's cost alone
-    if (__any(!ok) && N < 0) {
-#elif defined(CO_DIAG_CERT_TRIVIAL)
-    if (__any(!ok) && N < 0) {
-      lp += 1.f;
-    }
-    if (false) {
-#elif defined(CO_DIAG_CERT_STASHONLY)  // the certification and the stash, no fallback code
-    if (__any(!ok) && N < 0) {
-      asm volatile("" ::: "memory");
-      lp += stash[0];
-    }
-    if (false) {
-#else
     // rare (15 of 25,600 waves at the POMO timing shape): laid out after the hot path
     if (__builtin_expect(__any(!ok), 0)) {
-#endif
-      // the stash is re-read from LDS (a compiler barrier: forwarding the stored registers
-      // instead would keep EPL more VGPRs live through the fast path)
-      asm volatile("" ::: "memory");
       const int grp = lane_id() / RL;
       const uint64_t gmask = (RL == 64 ? ~0ull : ((1ull << RL) - 1ull)) << (grp * RL);
       const bool row_ok = (__ballot(!ok) & gmask) == 0ull;
@@ -720,28 +685,15 @@ __device__ __forceinline__ int greedy_row(GreedyRow<RL, EPL, VW>& g, bool valid,
       if (fix && !tier2) {
         lp = lw;
         sel = wi;
-#ifdef CO_DIAG_CERT_COUNT  // diagnostic only: marks the rows resolved by tier 1
-        lp = -23456.f;
-#endif
+        if constexpr (kDiagCertCount) lp = -23456.f;
       }
-      // Tier 2 (rarer still): the whole wave in the exact math from the stash (for the
-      // other rows the same action, their exact logp)
-#ifdef CO_DIAG_T2_NEVER  // timing diagnostic only: tier 2 compiled in but never taken
-      if (__any(tier2) && N < 0) {
-#else
+      // Tier 2 (rarer still): the whole wave in the exact math on the row read again (for
+      // the other rows the same action, their exact logp)
       if (__any(tier2)) {
-#endif
-#if !CO_CERT_STASH
         g.load(valid, N, lrow, mrow, c0);
-#else
-#pragma unroll
-        for (int k = 0; k < EPL; ++k) g.v[k] = stash[k];
-#endif
         L = g.template softmax_shift<OE, false>(clip, temp, N, sl, lds_row);
         sel = g.select(L, c0, lp);
-#ifdef CO_DIAG_CERT_COUNT  // diagnostic only: marks the rows of tier 2
-        if (tier2) lp = -12345.f;
-#endif
+        if (kDiagCertCount && tier2) lp = -12345.f;
       }
     }
     (void)lrow;
@@ -1228,7 +1180,7 @@ inline unsigned decode_grid(int64_t B, int N, int unr = 1) {
   const int rl = N <= 16 ? CO_RL16 : N <= 32 ? CO_RL32 : N <= 64 ? CO_RL64
                : N <= 128 ? CO_RL128 : N <= 256 ? CO_RL256 : 64;
   const int64_t waves = ((B + unr - 1) / unr * rl + 63) / 64;
-  return grid_for(waves, 4, (int64_t)1 << 30);  // every row group gets its wave
+  return cover_grid(waves, 4);  // every row group gets its wave; 0: B too large
 }
 
 // widest GreedyRow load (4 / 2 / 1 elements) the row length, stride and pointers allow

@@ -484,7 +484,8 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
   const SlapEpi epi{(int)P, to_choose, tc_stride, assign_in, assign_out, mask_out,
                     i_in,   i_out,     done,      step_reward, ll_accum};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((B + rpw * 4 - 1) / (rpw * 4))), block(256);
+  const dim3 grid(cover_grid(B, rpw * 4)), block(256);
+  if (grid.x == 0) return CO_E_INVAL;
   if (mode == CO_DECODE_GREEDY) {
 #define CO_SDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \
@@ -556,7 +557,8 @@ extern "C" int co_cvrp_decode_step(int64_t B, int64_t Ncust, const float* logits
   const CvrpEpi epi{(int)Ncust, demand,  used_in, used_out,    vcap,     vis_in,
                     vis_out,    cur_out, done,    step_reward, mask_out, ll_accum};
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((B + rpw * 4 - 1) / (rpw * 4))), block(256);
+  const dim3 grid(cover_grid(B, rpw * 4)), block(256);
+  if (grid.x == 0) return CO_E_INVAL;
   if (mode == CO_DECODE_GREEDY) {
 #define CO_CDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \

@@ -3,7 +3,7 @@
 // ranking.
 #include "decode_common.hpp"
 
-#if defined(CO_DIAG_FASTTANH) || defined(CO_DIAG_FASTEXP)
+#if defined(CO_DIAG_FASTTANH) || defined(CO_DIAG_FASTEXP)  // co_diag.hpp: kDiagTimingCut
 // timing-diagnostic build: the "exact" decode is not exact (see _native.load())
 extern "C" __attribute__((visibility("default"))) const int co_variant_timing_cut_decode = 1;
 #endif
@@ -43,6 +43,7 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
     return launch_status();
   }
   const dim3 grid(decode_grid(B, (int)N)), block(256);
+  if (grid.x == 0) return CO_E_INVAL;
   const bool filtered = (top_k > 0 && top_k < N) || (top_p > 0.0 && top_p < 1.0);
   if (mode == CO_DECODE_GREEDY && !filtered) {
 #define CO_GREEDY(RL, EPL, V)                                                                  \

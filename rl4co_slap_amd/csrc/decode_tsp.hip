@@ -22,6 +22,7 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
   hipStream_t s = (hipStream_t)stream;
   if (mode == CO_DECODE_GREEDY) {
     const dim3 grid(decode_grid(B, (int)N)), block(256);
+    if (grid.x == 0) return CO_E_INVAL;
 #define CO_TDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \
                     (tsp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), grid, block, 0, \
@@ -36,6 +37,7 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
     return launch_status();
   }
   const dim3 grid(decode_grid(B, (int)N, CO_DECODE_UNR)), block(256);
+  if (grid.x == 0) return CO_E_INVAL;
 #define CO_TDS(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH(hipLaunchKernelGGL, (tsp_decode_step_kernel<RL, EPL, V, OPT>), grid, block,   \
                   0, s, B, (int)N, logits, lstride, mask_in, clip, temp, mode, action_in,       \

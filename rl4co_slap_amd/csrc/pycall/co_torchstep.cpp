@@ -452,7 +452,8 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     if (fr.dim() < 2) Py_RETURN_NONE;
     const int64_t p = fr.size(fr.dim() - 2);
     if (logits.size(0) != b || logits.size(1) != l || l > 2048 || tc.size(0) != b ||
-        !fits(i, dev, at::kLong, b) || !fits(asg, dev, at::kInt, b * p) || asg.dim() != 2)
+        !fits(i, dev, at::kLong, b) || !fits(asg, dev, at::kInt, b * p) || asg.dim() != 2 ||
+        asg.size(0) != b)
       Py_RETURN_NONE;
     if (ain && !fits(*ain, dev, at::kLong, b)) Py_RETURN_NONE;
     const int64_t kb = up(8 * b);

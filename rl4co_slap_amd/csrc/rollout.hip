@@ -171,10 +171,6 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
   // launcher guarantees LB == B or LB % 64 == 0, so a tile never wraps
   stage_bytes_lds(reinterpret_cast<const unsigned char*>(locs + (row0 % LB) * N), rows * N * 8,
                   reinterpret_cast<unsigned char*>(s_xy));  // ends with a barrier
-#if defined(CO_DIAG_PHASE) && CO_DIAG_PHASE == 1
-  if (live && q == 0 && s_xy[lane].x == 12345.f) reward_out[b] = 1.f;
-  return;
-#endif
   const float2* xy = s_xy + lane * N;
   uint32_t* vw = s_vis + lane * VS;
   uint32_t badw = 0;
@@ -269,10 +265,6 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
       }
     }
   }
-#if defined(CO_DIAG_PHASE) && CO_DIAG_PHASE == 2
-  if (live && q == 0) reward_out[b] = -(float)len + (float)(vw[0] & 1) + (badw ? 1.f : 0.f);
-  return;
-#endif
   // out-of-range actions seen by this wave (revisits: from the final words below)
   if (__any(badw != 0u && check) && lane == 0) set_status(status, CO_ST_INVALID_TOUR);
   __syncthreads();  // steps done: the coordinate tile is free, the visited words final
@@ -915,7 +907,8 @@ int launch_tsp_teacher(int64_t B, int64_t N, const float2* l2, int64_t LB, const
   constexpr int Q = CO_TEACH_Q, PRE = CO_TEACH_NB;
   const int NW = NW_launch(N);
   const size_t shmem = tsp_tile_bytes((int)N, Q) + (size_t)64 * (2 * NW + 1) * 4;
-  const dim3 grid((unsigned)((B + 63) / 64)), block(64 * Q);
+  const dim3 grid(cover_grid(B, 64, 64 * Q)), block(64 * Q);
+  if (grid.x == 0) return CO_E_INVAL;
   // a wave's step range fits the register prefetch: R = ceil((N - 1) / Q) <= PRE * U
   const bool pre = PRE > 0 && (N - 1 + Q - 1) / Q <= PRE * CO_TEACH_U;
 #define CO_TEACH(W, P)                                                                         \
@@ -952,7 +945,8 @@ int launch_tsp_rows(int64_t B, int64_t N, const float2* l2, int64_t LB, const in
                       ((reinterpret_cast<uintptr_t>(acts) | reinterpret_cast<uintptr_t>(l2)) & 15) == 0;
 #define CO_ROWS(GG, EE)                                                                        \
   do {                                                                                         \
-    const dim3 grid((unsigned)(((B + 64 / GG - 1) / (64 / GG) + 3) / 4)), block(256);          \
+    const dim3 grid(cover_grid((B + 64 / GG - 1) / (64 / GG), 4)), block(256);                 \
+    if (grid.x == 0) return CO_E_INVAL;                                                        \
     const size_t dsh = 4 * tsp_rows_wave_bytes(64 / GG, (int)N);                               \
     /* the static visited bitmaps come on top of the dynamic staging (64 KiB default) */       \
     const size_t sbits = (size_t)4 * (64 / GG) * ((GG * EE + 31) / 32) * 4;                    \
@@ -1100,7 +1094,8 @@ extern "C" int co_slap_rollout(int64_t B, int64_t L, int64_t P, int64_t O, int64
   const size_t shmem =
       slap_asg_bytes(ipb, (int)P) + 4 * slap_wave_bytes(64 / G, 8, (int)L, (int)O, (int)K);
   if (shmem > 160 * 1024) return CO_E_INVAL;
-  const dim3 grid((unsigned)((B + ipb - 1) / ipb)), block(256);
+  const dim3 grid(cover_grid(B, ipb)), block(256);
+  if (grid.x == 0) return CO_E_INVAL;
   hipStream_t s = (hipStream_t)stream;
   const float2* l2 = reinterpret_cast<const float2*>(locs);
 #define CO_SLAP(GG, EPL, C)                                                                    \

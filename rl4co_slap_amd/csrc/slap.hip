@@ -505,7 +505,8 @@ extern "C" int co_slap_step(int64_t B, int64_t L, int64_t P, const int64_t* acti
   // L <= 256 and 4-B-aligned mask rows; else the 64-row byte tile
   if (CO_SLAP_GROUP_STEP && L % 4 == 0 && L <= 256 &&
       ((reinterpret_cast<uintptr_t>(mask_in) | reinterpret_cast<uintptr_t>(mask_out)) & 3) == 0) {
-    const dim3 grid((unsigned)((B + 15) / 16));
+    const dim3 grid(cover_grid(B, 16));
+    if (grid.x == 0) return CO_E_INVAL;
     const int ku = (int)((L / 4 + 15) / 16);
 #define CO_SLAP_GS(K)                                                                         \
   hipLaunchKernelGGL((slap_closest_step_kernel<K, false>), grid, dim3(256), 0,               \
@@ -523,7 +524,8 @@ extern "C" int co_slap_step(int64_t B, int64_t L, int64_t P, const int64_t* acti
   }
   SlapRowEpilogue epi{(int)P, to_choose, tc_stride, assign_out, i_in, i_out, done, reward,
                       status};
-  const unsigned grid = (unsigned)((B + kTileRows - 1) / kTileRows);
+  const unsigned grid = cover_grid(B, kTileRows, kTileThreads);
+  if (grid == 0) return CO_E_INVAL;
   hipLaunchKernelGGL(slap_step_kernel, dim3(grid), dim3(kTileThreads), 0, (hipStream_t)stream, B,
                      (int)L, action, mask_in, mask_out, assign_in, epi,
                      tile_vec_ok(mask_in, mask_out));
@@ -610,7 +612,8 @@ extern "C" int co_slap_closest_step(int64_t B, int64_t L, int64_t P, const float
     return co_slap_step(B, L, P, action_out, to_choose, tc_stride, assign_in, assign, mask_in,
                         mask_out, i_in, i_out, done, reward, status, stream);
   }
-  const dim3 grid((unsigned)((B + 15) / 16));
+  const dim3 grid(cover_grid(B, 16));
+  if (grid.x == 0) return CO_E_INVAL;
   const int units = (int)(L / 4), ku = (units + 15) / 16;
 #define CO_SLAP_CS(K)                                                                        \
   hipLaunchKernelGGL((slap_closest_step_kernel<K, true>), grid, dim3(256), 0, (hipStream_t)stream, \

@@ -300,7 +300,8 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
     const int W = (int)(N >> 2), WG = (W + CO_TSP_WPL - 1) / CO_TSP_WPL;
     const int G = WG <= 2 ? 2 : WG <= 4 ? 4 : WG <= 8 ? 8 : WG <= 16 ? 16 : WG <= 32 ? 32 : 64;
     const int64_t waves = (B * G + 64 * CO_TSP_UNR - 1) / (64 * CO_TSP_UNR);
-    const dim3 grid(grid_for(waves, 4, (int64_t)1 << 30));  // a wave per CO_TSP_UNR row groups
+    const dim3 grid(cover_grid(waves, 4));  // a wave per CO_TSP_UNR row groups
+    if (grid.x == 0) return CO_E_INVAL;
     const uint32_t* mi = reinterpret_cast<const uint32_t*>(mask_in);
     uint32_t* mo = reinterpret_cast<uint32_t*>(mask_out);
     hipStream_t s = (hipStream_t)stream;
@@ -316,7 +317,8 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
 #undef CO_TSG
     return launch_status();
   }
-  const unsigned grid = (unsigned)((B + kTileRows - 1) / kTileRows);
+  const unsigned grid = cover_grid(B, kTileRows, kTileThreads);
+  if (grid == 0) return CO_E_INVAL;
   hipLaunchKernelGGL(tsp_step_kernel, dim3(grid), dim3(kTileThreads), 0, (hipStream_t)stream, B,
                      (int)N, action, mask_in, mask_out, epi, first_mode, first_flag, status, vec);
   return launch_status();

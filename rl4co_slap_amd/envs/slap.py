@@ -216,6 +216,12 @@ class SLAPEnv(RL4COEnvBase):
                 or tc.shape[-1] == 0 or tc.dtype != torch.float32):
             return None
         p = td["freq"].shape[-2]
+        # the operands the kernel indexes: i [b] int64, assignment [b, P] (it writes r*P + c)
+        if (i.dtype != torch.int64 or i.numel() != b or assign.dim() != 2
+                or tuple(assign.shape) != (b, p) or tc.shape[0] != b):
+            return None
+        if action_in is not None and action_in.numel() != b:
+            return None
         m, i, assign = mask.contiguous(), i.contiguous(), assign.contiguous()
         ain = action_in.long().contiguous() if action_in is not None else None
         s = nat.stream_of(m)

@@ -192,8 +192,8 @@ class TSPFusedEpisode(_GraphEpisode):
             assert actions is not None and actions.shape == (b, n)
             # the episode owns its copy (the transposed layout always copied): a captured
             # graph replays on these, whatever the caller later does to its tensor
-            self.acts = (actions.long().contiguous().clone() if self.rows
-                         else actions.t().contiguous())
+            self.acts = (actions.to(torch.long, memory_format=torch.contiguous_format, copy=True)
+                         if self.rows else actions.t().contiguous())
         else:
             self.acts = torch.empty((n, b), dtype=torch.int64, device=d)
         self.mask = torch.empty((b, n), dtype=torch.bool, device=d)

@@ -124,8 +124,11 @@ def global_metrics(bl: torch.Tensor, max_reward: torch.Tensor, loss_terms: torch
     read.  Without it the shard sizes are all-gathered first (a second collective and a
     host read per rank)."""
     local = torch.stack([bl, max_reward, loss_terms])  # [3, B_local]
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    if world > 1:
+    # with a process group the exchange always runs (at world size 1 too: the same RCCL /
+    # gloo call path, a copy of the local values); without one the values are local
+    grouped = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if grouped else 1
+    if grouped:
         if total_instances is not None:
             rank = dist.get_rank(group)
             sizes = [hi - lo for lo, hi in (shard_range(total_instances, world, r)

@@ -130,6 +130,22 @@ def random_policy(td):
     return td
 
 
+def _own_step(env) -> bool:
+    """True when ``env``'s ``_step`` is the one its ``decode_and_step`` fuses: the class
+    that defines ``decode_and_step`` (and ``native_decode_and_step``) must also be the one
+    whose ``_step`` the env runs.  A subclass that overrides ``_step`` (a CVRPTW- or
+    SDVRP-like env on top of CVRPEnv) inherits the fused call but not its transition, so
+    it takes the two-call path."""
+    cls = type(env)
+    if "_step" in getattr(env, "__dict__", {}):  # replaced on the instance
+        return False
+    for name in ("decode_and_step", "native_decode_and_step"):
+        owner = next((c for c in cls.__mro__ if name in c.__dict__), None)
+        if owner is not None and getattr(cls, "_step", None) is not owner.__dict__.get("_step"):
+            return False
+    return True
+
+
 def rollout(env, td, policy, max_steps: int = None):
     """``decoding.py:88-109``."""
     max_steps = float("inf") if max_steps is None else max_steps
@@ -274,7 +290,8 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         if cached is None or cached[0] is not env:
             fused = getattr(env, "decode_and_step", None)
             mode = self._mode()
-            if (fused is None or _NO_FUSED or self.store_all_logp or self.improvement_method_mode
+            if (fused is None or not _own_step(env) or _NO_FUSED or self.store_all_logp
+                    or self.improvement_method_mode
                     or self.top_k > 0 or 0.0 < self.top_p < 1.0 or not self.mask_logits
                     or mode not in _MODES):
                 fused = None

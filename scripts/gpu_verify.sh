@@ -1,4 +1,4 @@
-# Round 4 last check on the final tree: the whole GPU suite and smoke().
+# Last check on the final tree: the whole GPU suite and smoke().
 cd $GRAFT_REPO_ROOT
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
   > gpurun_out/verify_tests.log 2>&1
