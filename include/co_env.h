@@ -43,6 +43,7 @@ extern "C" {
 #define CO_ST_INFEASIBLE 4        /* "infeasible action selected" decoding.py:376-379 */
 #define CO_ST_INDEX_RANGE 8       /* index out of range (torch raises IndexError/RuntimeError) */
 #define CO_ST_TRUNCATED 16        /* an episode hit max_steps before done (rollout max_steps) */
+#define CO_ST_LOGP_NEG_INF 32     /* "Logprobs should not be -inf, ..."  decoding.py:57-58 */
 
 /* Library identification: returns the gfx target string compiled in. */
 const char* co_build_info(void);
@@ -123,15 +124,22 @@ int co_cvrp_reward(int64_t batch, int64_t num_loc, int64_t steps, const float* l
 
 /* SLAPEnv._reset (rl4co/envs/warehousing/slap/env.py:95-129). L = n_aisles*n_locs,
  * P = products: action_mask[B,L] = 1 except column 0 (depot); to_choose[B,P] =
- * 0..P-1 (float); i[B,1] = 0; reward[B,1] = 0; ratio[B,L] = 0 (ratio may be NULL). */
+ * 0..P-1 (float); i[B,1] = 0; reward[B,1] = 0; ratio[B,L] = 0 (ratio may be NULL); and
+ * the zero done[B,1] / terminated[B,1] that RL4COEnvBase.reset adds (envs/common/base.py:
+ * 138-143 via TorchRL; each may be NULL), so a reset is one launch. */
 int co_slap_reset(int64_t batch, int64_t num_slots, int64_t n_products, uint8_t* action_mask,
-                  float* to_choose, int64_t* i, float* reward, float* ratio, void* stream);
+                  float* to_choose, int64_t* i, float* reward, float* ratio, uint8_t* done,
+                  uint8_t* terminated, void* stream);
 
 /* SLAPEnv._step (slap/env.py:38-93): product p = (int)to_choose[b*tc_stride];
  * assign_out = assign_in with [b, p] = (int)action[b] (in-place allowed:
  * then only that element is written); mask_out = mask_in with [b, action] = 0
  * (in-place allowed); done[b] = (i_in[b] == P-1); reward[b] = 0 (bool);
- * i_out = i_in + 1.  Negative indices wrap like torch advanced indexing. */
+ * i_out = i_in + 1.  Negative indices wrap like torch advanced indexing.
+ * to_choose may be NULL when every row's to_choose[b, 0] holds one value k (the env's
+ * untouched arange to_choose at step k, slap/env.py:105-108): tc_stride then carries k
+ * (0 <= k < P) and no to_choose column is read (the same for co_slap_decode_step and
+ * co_slap_closest_step). */
 int co_slap_step(int64_t batch, int64_t num_slots, int64_t n_products, const int64_t* action,
                  const float* to_choose, int64_t tc_stride, const int32_t* assign_in,
                  int32_t* assign_out, const uint8_t* mask_in, uint8_t* mask_out,
@@ -438,6 +446,18 @@ int co_randint_fill(int64_t* out, int64_t n, int64_t low, int64_t high, uint64_t
  * full grid -- the streaming ceiling the bench quotes beside each kernel's roofline.
  * src/dst 16-byte aligned, nbytes a multiple of 16. */
 int co_probe_copy(const void* src, void* dst, int64_t nbytes, void* stream);
+
+/* The decode loop's epilogue (DecodingStrategy.post_decoder_hook, decoding.py:315-325, and
+ * get_log_likelihood, decoding.py:39-65) in one launch.  The T per-step [B] actions and
+ * log-probabilities are rows of step-major slabs (act_sm[t * act_rs + b], logp_sm[t *
+ * logp_rs + b]: the tensors the per-step calls returned); writes torch.stack(..., 1) =
+ * actions[B, T] / logprobs[B, T], ll[B] = logprobs.sum(1) (summed in step order in f64,
+ * rounded once; may be NULL), and ORs CO_ST_LOGP_NEG_INF into status when any log-
+ * probability is not > -1000 (the assert of decoding.py:57-58).  act_sm or logp_sm may be
+ * NULL (that half is skipped). */
+int co_episode_stack(int64_t batch, int64_t steps, const int64_t* act_sm, int64_t act_rs,
+                     const float* logp_sm, int64_t logp_rs, int64_t* actions, float* logprobs,
+                     float* ll, int32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

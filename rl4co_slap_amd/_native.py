@@ -32,7 +32,7 @@ _SIGS = {
     "co_cvrp_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "co_cvrp_action_mask": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p],
     "co_cvrp_reward": [_i64, _i64, _i64, _p, _p, _i64, _i64, _p, _p, _i32, _p, _p, _p],
-    "co_slap_reset": [_i64, _i64, _i64, _p, _p, _p, _p, _p, _p],
+    "co_slap_reset": [_i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
     "co_slap_step": [_i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     "co_slap_reward": [_i64, _i64, _i64, _i64, _i64, _p, _p, _p, _p, _p, _p],
     "co_gather_by_index": [_p, _i64, _i64, _i64, _i64, _i64, _p, _i64, _i64, _i64, _p, _p, _p],
@@ -53,6 +53,7 @@ _SIGS = {
     "co_count_not_done": [_p, _i64, _p, _p],
     "co_row_deficit_max": [_p, _i64, _i64, _i64, _p, _p],
     "co_probe_copy": [_p, _p, _i64, _p],
+    "co_episode_stack": [_i64, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p],
     "co_uniform_fill": [_p, _i64, _f32, _f32, _f32, _i32, _u64, _u64, _p],
     "co_randint_fill": [_p, _i64, _i64, _i64, _u64, _u64, _p],
     "co_pomo_shared_baseline": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p],
@@ -79,6 +80,7 @@ ST_OVER_CAPACITY = 2
 ST_INFEASIBLE = 4
 ST_INDEX_RANGE = 8
 ST_TRUNCATED = 16
+ST_LOGP_NEG_INF = 32
 DECODE_FAST = 0x100  # CO_DECODE_FAST mode flag (opt-in fast math; not bit-exact)
 DECODE_CERTIFIED = 0x200  # CO_DECODE_CERTIFIED: fast math, greedy actions certified exact
 
@@ -311,6 +313,9 @@ class _TorchStep:
         self.cvrp_step = bound(mod.cvrp_step, "co_cvrp_step")
         self.slap_step_td = bound(mod.slap_step_td, "co_slap_decode_step")
         self.cvrp_step_td = bound(mod.cvrp_step_td, "co_cvrp_decode_step")
+        self.slap_reset_td = bound(mod.slap_reset_td, "co_slap_reset")
+        self.episode_stack = bound(mod.episode_stack, "co_episode_stack")
+        self.slab_fresh = mod.slab_fresh
         self.clear_pool = mod.clear_pool
 
 
@@ -379,9 +384,30 @@ def bind(name, *args):
     return launch
 
 
-def scratch_status(device) -> torch.Tensor:
-    """A zeroed device int32 word for data-dependent error bits."""
-    return torch.zeros(1, dtype=torch.int32, device=device)
+_zero_words = {}  # (device type, index, words) -> status tensors a host read found all zero
+
+
+def scratch_status(device, words: int = 1) -> torch.Tensor:
+    """``words`` zeroed int32 words for data-dependent error bits.  A status tensor whose
+    host read found every word zero (``release_status``: the read synchronised, nothing
+    writes it since) is handed out again instead of zero-filling a new one -- a fill is a
+    kernel launch, ~4 us of host time on an episode's fixed path."""
+    device = torch.device(device)
+    free = _zero_words.get((device.type, device.index, words))
+    if free:
+        return free.pop()
+    return torch.zeros(words, dtype=torch.int32, device=device)
+
+
+def release_status(t: torch.Tensor, values) -> None:
+    """Return a status tensor to the zero pool after a host read of it (``values``) found
+    no bit set; the caller must not use it afterwards."""
+    if any(values) or t.dim() != 1 or t._base is not None:
+        return
+    d = t.device
+    free = _zero_words.setdefault((d.type, d.index, t.shape[0]), [])
+    if len(free) < 8:
+        free.append(t)
 
 
 # Per-device word that kernels without a caller-held status (gather_by_index) OR their

@@ -72,7 +72,8 @@ struct SlapStage {
   __device__ __forceinline__ void issue(const SlapEpi& e, int64_t base, int nr) const {
     const int Pn = P;
     dma_dwords(2 * nr, s, [&](int k) { return reinterpret_cast<const uint32_t*>(e.i_in + base) + k; });
-    dma_dwords(nr, s + 2 * RPW, [&](int k) { return e.to_choose + (base + k) * e.tc_stride; });
+    if (e.to_choose)  // else the uniform product e.tc_stride: no strided 4-B reads
+      dma_dwords(nr, s + 2 * RPW, [&](int k) { return e.to_choose + (base + k) * e.tc_stride; });
     if (e.ll_accum) dma_dwords(nr, s + 3 * RPW, [&](int k) { return e.ll_accum + base + k; });
     if (e.assign_in != e.assign_out)
       dma_dwords(nr * Pn, s + 4 * RPW, [&](int k) { return e.assign_in + base * Pn + k; });
@@ -91,7 +92,8 @@ struct SlapStage {
   // advanced-index write raises).
   __device__ __forceinline__ bool store(const SlapEpi& e, int64_t r, int g, int sl,
                                         int64_t a_raw) const {
-    int64_t p = (int64_t)(int)prod_of(g);  // .to(torch.int), slap/env.py:52
+    // .to(torch.int), slap/env.py:52; to_choose NULL: every row's product is tc_stride
+    int64_t p = e.to_choose ? (int64_t)(int)prod_of(g) : e.tc_stride;
     if (p < 0) p += e.P;
     const bool p_ok = p >= 0 && p < e.P;
     const int32_t av_new = (int32_t)a_raw;  // .to(torch.int), slap/env.py:53-54
@@ -461,16 +463,16 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
   mode &= ~(CO_DECODE_FAST | CO_DECODE_CERTIFIED);
   if (mode < 0 || mode > 2) return CO_E_MODE;
   if (B == 0) return CO_OK;
-  if (!logits || !mask_in || !action_out || !to_choose || !assign_in || !assign_out ||
-      !mask_out || !i_in || !i_out || !done || !step_reward ||
-      (mode == CO_DECODE_EVALUATE && !action_in))
+  if (!logits || !mask_in || !action_out || !assign_in || !assign_out || !mask_out || !i_in ||
+      !i_out || !done || !step_reward || (mode == CO_DECODE_EVALUATE && !action_in) ||
+      (!to_choose && (tc_stride < 0 || tc_stride >= P)))
     return CO_E_INVAL;
   if (mask_out == mask_in) return CO_E_INVAL;  // the mask is read by other lanes' decode
   const int64_t N = L;  // the row-dispatch macros' name for the row length
   const int rpw = 64 / row_lanes(N);
   const size_t shmem = (size_t)4 * slap_stage_dwords(rpw, (int)P) * 4;
   const size_t lds_static = (size_t)4 * 64 * row_epl(N) * 4;
-  if (shmem + lds_static > 64 * 1024 || !aligned4(to_choose) || !aligned4(assign_in) ||
+  if (shmem + lds_static > 64 * 1024 || (to_choose && !aligned4(to_choose)) || !aligned4(assign_in) ||
       !aligned4(i_in) || (ll_accum && !aligned4(ll_accum))) {
     // beyond the stage (huge P) or misaligned: the two launches it fuses
     if (ll_accum) return CO_E_INVAL;

@@ -408,7 +408,8 @@ CO_HOST_API int co_cvrp_reward(int64_t B, int64_t N, int64_t T, const float* loc
 // ---------------------------------------------------------------------------- SLAP
 // slap/env.py:95-129
 CO_HOST_API int co_slap_reset(int64_t B, int64_t L, int64_t P, uint8_t* mask, float* to_choose,
-                              int64_t* it, float* reward, float* ratio, void*) {
+                              int64_t* it, float* reward, float* ratio, uint8_t* done,
+                              uint8_t* terminated, void*) {
   if (B < 0 || L <= 0 || P <= 0) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!mask || !to_choose || !it || !reward) return CO_E_INVAL;
@@ -419,6 +420,8 @@ CO_HOST_API int co_slap_reset(int64_t B, int64_t L, int64_t P, uint8_t* mask, fl
       for (int64_t l = 0; l < L; ++l) ratio[b * L + l] = 0.f;
     it[b] = 0;
     reward[b] = 0.f;
+    if (done) done[b] = 0;
+    if (terminated) terminated[b] = 0;
   }
   return CO_OK;
 }
@@ -431,8 +434,8 @@ CO_HOST_API int co_slap_step(int64_t B, int64_t L, int64_t P, const int64_t* act
                              int32_t* status, void*) {
   if (B < 0 || L <= 0 || P <= 0 || L > (1 << 30)) return CO_E_INVAL;
   if (B == 0) return CO_OK;
-  if (!action || !to_choose || !assign_in || !assign_out || !mask_in || !mask_out || !i_in ||
-      !i_out || !done || !reward)
+  if (!action || !assign_in || !assign_out || !mask_in || !mask_out || !i_in || !i_out ||
+      !done || !reward || (!to_choose && (tc_stride < 0 || tc_stride >= P)))
     return CO_E_INVAL;
   for (int64_t b = 0; b < B; ++b) {
     if (assign_out != assign_in)
@@ -444,7 +447,8 @@ CO_HOST_API int co_slap_step(int64_t B, int64_t L, int64_t P, const int64_t* act
       set_status(status, CO_ST_INDEX_RANGE);
     else
       mask_out[b * L + a] = 0;
-    int64_t p = (int64_t)(int)to_choose[b * tc_stride];  // .to(torch.int), env.py:52
+    // .to(torch.int), env.py:52; to_choose NULL: the uniform product tc_stride
+    int64_t p = to_choose ? (int64_t)(int)to_choose[b * tc_stride] : tc_stride;
     if (p < 0) p += P;
     if (p < 0 || p >= P)
       set_status(status, CO_ST_INDEX_RANGE);

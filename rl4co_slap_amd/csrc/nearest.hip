@@ -18,6 +18,14 @@ namespace {
 
 constexpr int kNoNode = 0x7fffffff;
 
+// a constant materialised in a scalar register at its use (an empty asm with an "s"
+// operand): hoisted out of the step loop, the loop's constants otherwise hold VGPRs for
+// the whole kernel, and the CVRP episode needs <= 64 of them for 8 waves per SIMD
+__device__ __forceinline__ uint32_t su(uint32_t c) {
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
 // Lane-local nearest candidate: argmin over the candidates (bit k of `cand`) of the f32
 // distance sqrt(dx*dx + dy*dy), ties -> lowest node index, exactly as torch.argmin over
 // the oracle's distances.  The scan compares squared distances (the same IEEE products
@@ -54,7 +62,64 @@ __device__ __forceinline__ void lane_nearest(float cx, float cy, const float (&p
   }
 }
 
-// TSP: step 0 takes node 0, steps 1..N-1 the nearest unvisited node.
+// The group's nearest candidate, exactly as lane_nearest + grp_argmin_split, with the
+// common case on squared distances only: each lane scans its candidates once (the first
+// index of its smallest squared distance, strict <, and sbef = the smallest before it),
+// the group min of the squared distances is one integer DPP min per stage (non-negative
+// f32 order as their bit patterns), and the winner is the lowest node index holding it.
+// The f32 sqrt can merge squared distances within a relative 2^-22: when some candidate
+// other than the winner lies within 2^-20 of the minimum at a lower index, or before its
+// lane's best (rare), the wave redoes the step with the per-lane correctly rounded sqrt
+// (lane_nearest, grp_argmin_split).  Returns the winning node (kNoNode: no candidate)
+// and its squared distance m (+inf: none); every lane of the wave must take part.
+template <int G, int EPL>
+__device__ __forceinline__ int grp_nearest(float cx, float cy, const float (&px)[EPL],
+                                           const float (&py)[EPL], uint32_t cand, int sl,
+                                           float& m) {
+  const float inf = __uint_as_float(su(0x7f800000u));
+  float smin = inf, sbef = inf;
+  int kmin = -1;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const float dx = px[k] - cx, dy = py[k] - cy;
+    const float sq = dx * dx + dy * dy;
+    const bool take = ((cand >> k) & 1u) && sq < smin;
+    sbef = take ? smin : sbef;
+    smin = take ? sq : smin;
+    kmin = take ? k : kmin;
+  }
+  const uint32_t mb = grp_reduce<G>(__float_as_uint(smin), [](uint32_t a, uint32_t b) {
+    return a < b ? a : b;
+  });
+  const int none = (int)su((uint32_t)kNoNode);
+  const int my = kmin >= 0 ? sl + G * kmin : none;
+  int w = grp_min_int<G>(__float_as_uint(smin) == mb ? my : none);
+  m = __uint_as_float(mb);
+  const float win = m * (1.0f + 0x1p-20f);
+  const bool near = mb < su(0x7f800000u) && ((smin <= win && my < w) || sbef <= win);
+  if (__builtin_expect(__any(near), 0)) {  // a tie of the rounded distances: exact path
+    float best;
+    int bi;
+    lane_nearest<G, EPL>(cx, cy, px, py, cand, sl, best, bi);
+    grp_argmin_split<G>(best, bi);
+    w = bi;  // m stays: the winner's distance rounds to sqrtf(m)
+  }
+  return w;
+}
+
+// The group's value from lane `owner` (`v` of the other lanes is ignored): an OR over the
+// group of the owner's bits, DPP only.
+template <int G>
+__device__ __forceinline__ float grp_from(float v, bool mine) {
+  return __uint_as_float(grp_reduce<G>(mine ? __float_as_uint(v) : 0u,
+                                       [](uint32_t a, uint32_t b) { return a | b; }));
+}
+
+// TSP: step 0 takes node 0, steps 1..N-1 the nearest unvisited node.  One group of G
+// lanes per instance, 64/G per wave, one wave's instances per 64/G rows of the grid (no
+// grid-stride loop: nothing is hoisted across instances, so the kernel stays within 64
+// VGPRs -- 8 waves per SIMD); the group's coordinate row in LDS (8 B per node) gives the
+// chosen node's coordinates as one broadcast read.
 template <int G, int EPL>
 __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
     int64_t B, int N, const float2* __restrict__ locs, int64_t* __restrict__ acts_out,
@@ -62,70 +127,59 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
     int64_t* __restrict__ cur_out, int64_t* __restrict__ i_out, uint8_t* __restrict__ done_out,
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out) {
   constexpr int IPW = 64 / G;
-  // the group's coordinate row in LDS: the chosen node's coordinates are one broadcast
-  // ds_read per step instead of an EPL-wide register select and two lane shuffles
   __shared__ float2 s_xy[256 * EPL];
   const int lane = lane_id(), sl = lane % G;
   float2* xyg = s_xy + (threadIdx.x / G) * (G * EPL);
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * IPW; base < B; base += nwaves * IPW) {
-    const int64_t b = base + lane / G;
-    const bool valid = b < B;
-    const int64_t bb = valid ? b : 0;
-    const float2* lrow = locs + bb * N;
-    float px[EPL], py[EPL];
-    uint32_t vis = 0;  // bit k: node sl + G*k visited (or past N)
+  const int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * IPW;
+  if (base >= B) return;  // wave-uniform
+  const int64_t b = base + lane / G;
+  const bool valid = b < B;
+  const int64_t bb = valid ? b : B - 1;  // a dead group mirrors the last instance
+  const float2* lrow = locs + bb * N;
+  float px[EPL], py[EPL];
+  uint32_t vis = 0;  // bit k: node sl + G*k visited (or past N)
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const int c = sl + G * k;
-      const float2 q = c < N ? lrow[c] : make_float2(0.f, 0.f);
-      px[k] = q.x;
-      py[k] = q.y;
-      xyg[c] = q;
-      if (c >= N) vis |= 1u << k;
-    }
-    // the row is written and read by lanes of this wave only: a wave-level fence
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (sl == 0) vis |= 1u;  // step 0: node 0
-    const float2 p0 = xyg[0];
-    const float x0 = p0.x, y0 = p0.y;
-    float cx = x0, cy = y0;
-    if (valid && sl == 0) acts_out[bb] = 0;
-    double len = 0.0;
-    int cur = 0;
-    for (int t = 1; t < N; ++t) {
-      float best;
-      int bi;
-      lane_nearest<G, EPL>(cx, cy, px, py, ~vis, sl, best, bi);
-      grp_argmin_split<G>(best, bi);  // t < N: an unvisited node remains
-      const int owner = bi % G, slot = bi / G;
-      if (sl == owner) vis |= 1u << slot;
-      const float2 q = xyg[bi];
-      cx = q.x;
-      cy = q.y;
-      len += (double)best;
-      cur = bi;
-      if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = bi;
-    }
-    len += (double)edge_len(cx, cy, x0, y0);
-    // the next instance's row overwrites this one: order the reads above before it
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (!valid) continue;
-    uint8_t* mrow = mask_out + bb * N;
-    for (int c = sl; c < N; c += G) mrow[c] = 0;  // every node visited
-    if (sl == 0) {
-      first_out[bb] = 0;
-      cur_out[bb] = cur;
-      i_out[bb] = N;
-      done_out[bb] = 1;
-      step_reward_out[bb] = 0;
-      reward_out[bb] = -(float)len;
-    }
+  for (int k = 0; k < EPL; ++k) {
+    const int c = sl + G * k;
+    const float2 q = c < N ? lrow[c] : make_float2(0.f, 0.f);
+    px[k] = q.x;
+    py[k] = q.y;
+    xyg[c] = q;
+    if (c >= N) vis |= 1u << k;
+  }
+  // the row is written and read by lanes of this wave only: a wave-level fence
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (sl == 0) vis |= 1u;  // step 0: node 0
+  const float x0 = px[0], y0 = py[0];  // node 0 is lane 0's slot 0: broadcast it
+  float cx = __shfl(x0, lane - sl, 64), cy = __shfl(y0, lane - sl, 64);
+  const float fx = cx, fy = cy;
+  if (valid && sl == 0) acts_out[bb] = 0;
+  double len = 0.0;
+  int cur = 0;
+  for (int t = 1; t < N; ++t) {
+    float m;
+    const int a = grp_nearest<G, EPL>(cx, cy, px, py, ~vis, sl, m);  // t < N: one is left
+    if (sl == a % G) vis |= 1u << (a / G);
+    const float2 q = xyg[a];
+    cx = q.x;
+    cy = q.y;
+    len += (double)__builtin_sqrtf(m);
+    cur = a;
+    if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
+  }
+  len += (double)edge_len(cx, cy, fx, fy);
+  if (!valid) return;
+  uint8_t* mrow = mask_out + bb * N;
+  for (int c = sl; c < N; c += G) mrow[c] = 0;  // every node visited
+  if (sl == 0) {
+    first_out[bb] = 0;
+    cur_out[bb] = cur;
+    i_out[bb] = N;
+    done_out[bb] = 1;
+    step_reward_out[bb] = 0;
+    reward_out[bb] = -(float)len;
   }
 }
 
@@ -135,6 +189,9 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
 // (a != 0), done = every node visited (visited.sum == N + 1, so the depot must have
 // been entered once).  A finished instance stops; co_cvrp_rollout's pad pass then
 // applies the reference's remaining depot steps up to the batch-wide episode length.
+// Coordinates and demand in VGPRs; the chosen node's coordinates from the group's LDS
+// row (8 B per node: with 4 KB of LDS per wave, 8 waves fit per SIMD), its demand from
+// the owner lane's register by a group OR.
 template <int G, int EPL>
 __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
     int64_t B, int N, const float2* __restrict__ depot, const float2* __restrict__ locs_in,
@@ -145,110 +202,109 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out,
     int32_t* __restrict__ len_out, int32_t* __restrict__ tmax, int32_t* status) {
   constexpr int IPW = 64 / G;
-  // the group's nodes (x, y, demand) in LDS: the chosen node is one broadcast ds_read
-  __shared__ float4 s_node[256 * EPL];
+  __shared__ float2 s_xy[256 * EPL];
   const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
-  float4* ndg = s_node + (threadIdx.x / G) * (G * EPL);
+  float2* xyg = s_xy + (threadIdx.x / G) * (G * EPL);
   const int M = N + 1;
-  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  for (int64_t base = wid * IPW; base < B; base += nwaves * IPW) {
-    const int64_t b = base + lane / G;
-    const bool valid = b < B;
-    const int64_t bb = valid ? b : 0;
-    const float2* lrow = locs_in + bb * N;
-    const float* drow = demand + bb * N;
-    const float2 dep = depot[bb];
-    float px[EPL], py[EPL], dm[EPL];
-    uint32_t vis = 0;  // bit k: node sl + G*k visited (or past N)
+  const int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * IPW;
+  if (base >= B) return;  // wave-uniform
+  const int64_t b = base + lane / G;
+  const bool valid = b < B;
+  const int bb = (int)(valid ? b : B - 1);  // a dead group mirrors the last instance
+  const float2* lrow = locs_in + (int64_t)bb * N;
+  const float* drow = demand + (int64_t)bb * N;
+  const float2 dep = depot[bb];
+  float px[EPL], py[EPL], dm[EPL];
+  uint32_t vis = 0;  // bit k: node sl + G*k visited (or past N)
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const int c = sl + G * k;
+    float2 q = make_float2(0.f, 0.f);
+    float d = 0.f;
+    if (c == 0) {
+      q = dep;
+    } else if (c <= N) {
+      q = lrow[c - 1];
+      d = drow[c - 1];
+    }
+    px[k] = q.x;
+    py[k] = q.y;
+    dm[k] = d;
+    xyg[c] = q;
+    if (c > N) vis |= 1u << k;
+    if (valid && locs_out && c <= N) locs_out[(int64_t)bb * M + c] = q;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  float cx = dep.x, cy = dep.y, used = 0.f;
+  // packed group-uniform counters (register pressure: 8 waves per SIMD need <= 64 VGPRs):
+  // st = customers visited (bits 0-15) | steps taken (bits 16-30) | depot entered (bit 31)
+  uint32_t st = 0;
+  int cur = 0;
+  bool done = false;
+  double dist = 0.0;
+  for (int t = 0; t < max_steps; ++t) {
+    if (__ballot(!done) == 0) break;  // wave-uniform: the group reductions need every lane
+    uint32_t cand = 0;
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
       const int c = sl + G * k;
-      float2 q = make_float2(0.f, 0.f);
-      float d = 0.f;
-      if (c == 0) {
-        q = dep;
-      } else if (c <= N) {
-        q = lrow[c - 1];
-        d = drow[c - 1];
-      }
-      px[k] = q.x;
-      py[k] = q.y;
-      dm[k] = d;
-      ndg[c] = make_float4(q.x, q.y, d, 0.f);
-      if (c > N) vis |= 1u << k;
-      if (valid && locs_out && c <= N) locs_out[bb * M + c] = q;
+      const bool feas = c >= 1 && !((vis >> k) & 1u) && !(dm[k] + used > vcap);
+      cand |= (uint32_t)feas << k;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float cx = dep.x, cy = dep.y, used = 0.f;
-    int cur = 0, ncust = 0, len = 0;
-    bool depot_seen = false, done = false;
-    double dist = 0.0;
-    for (int t = 0; t < max_steps; ++t) {
-      if (__ballot(!done) == 0) break;  // wave-uniform: the group reductions need every lane
-      uint32_t cand = 0;
+    float m;
+    const int bi = grp_nearest<G, EPL>(cx, cy, px, py, cand, sl, m);
+    const int a = bi == kNoNode ? 0 : bi;
+    const int owner = a % G, slot = a / G;
+    float dsel = 0.f;  // the owner lane's demand of node a
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) {
-        const int c = sl + G * k;
-        const bool feas = c >= 1 && !((vis >> k) & 1u) && !(dm[k] + used > vcap);
-        cand |= (uint32_t)feas << k;
-      }
-      float best;
-      int bi;
-      lane_nearest<G, EPL>(cx, cy, px, py, cand, sl, best, bi);
-      grp_argmin_split<G>(best, bi);
-      if (done) continue;
-      const int a = bi == kNoNode ? 0 : bi;
-      const int owner = a % G, slot = a / G;
-      const float4 nd = ndg[a];
-      const float ax = nd.x, ay = nd.y, ad = nd.z;
-      if (sl == owner) vis |= 1u << slot;
-      dist += (double)(a == 0 ? edge_len(cx, cy, ax, ay) : best);
-      used = a != 0 ? (used + ad) * 1.0f : 0.0f;  // cvrp/env.py:83-85
-      ncust += a != 0;
-      depot_seen |= a == 0;
-      cur = a;
-      cx = ax;
-      cy = ay;
-      if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
-      len = t + 1;
-      done = ncust == N && depot_seen;
-    }
-    dist += (double)edge_len(cx, cy, dep.x, dep.y);  // closing edge to the depot
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // next row overwrites this one
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // final state rows: visited and get_action_mask (cvrp/env.py:137-149)
-    bool any_feas = false;
-    uint8_t* vrow = visited_out + bb * M;
-    uint8_t* mrow = mask_out + bb * M;
+    for (int k = 0; k < EPL; ++k) dsel = k == slot ? dm[k] : dsel;
+    const float ad = grp_from<G>(dsel, sl == owner);
+    if (done) continue;
+    if (sl == owner) vis |= 1u << slot;
+    const float2 q = xyg[a];
+    const float dx = q.x - cx, dy = q.y - cy;  // = m for a customer (same operations)
+    dist += (double)__builtin_sqrtf(dx * dx + dy * dy);
+    used = a != 0 ? (used + ad) * 1.0f : 0.0f;  // cvrp/env.py:83-85
+    st = ((st & 0x8000ffffu) + (a != 0 ? 1u : 0u)) | ((uint32_t)(t + 1) << 16) |
+         (a == 0 ? 0x80000000u : 0u);
+    cur = a;
+    cx = q.x;
+    cy = q.y;
+    if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
+    done = (st & 0x8000ffffu) == (0x80000000u | (uint32_t)N);
+  }
+  const int len = (int)((st >> 16) & 0x7fffu);
+  dist += (double)edge_len(cx, cy, dep.x, dep.y);  // closing edge to the depot
+  // final state rows: visited and get_action_mask (cvrp/env.py:137-149)
+  bool any_feas = false;
+  uint8_t* vrow = visited_out + (int64_t)bb * M;
+  uint8_t* mrow = mask_out + (int64_t)bb * M;
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const int c = sl + G * k;
-      const bool v = (vis >> k) & 1u;
-      const bool feas = c >= 1 && c <= N && !v && !(dm[k] + used > vcap);
-      any_feas |= feas;
-      if (valid && c <= N) {
-        vrow[c] = v;
-        if (c >= 1) mrow[c] = feas;
-      }
+  for (int k = 0; k < EPL; ++k) {
+    const int c = sl + G * k;
+    const bool v = (vis >> k) & 1u;
+    const bool feas = c >= 1 && c <= N && !v && !(dm[k] + used > vcap);
+    any_feas |= feas;
+    if (valid && c <= N) {
+      vrow[c] = v;
+      if (c >= 1) mrow[c] = feas;
     }
-    const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
-    const bool anyf = (__ballot(any_feas) & gmask) != 0;
-    if (valid && sl == 0) {
-      mrow[0] = !((cur == 0) && anyf);
-      cur_out[bb] = cur;
-      used_out[bb] = used;
-      vcap_out[bb] = vcap;
-      done_out[bb] = done;
-      step_reward_out[bb] = 0;
-      reward_out[bb] = -(float)dist;
-      len_out[bb] = len;
-      if (!done) set_status(status, CO_ST_TRUNCATED);
-      atomicMax(tmax, len);
-    }
+  }
+  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+  const bool anyf = (__ballot(any_feas) & gmask) != 0;
+  if (valid && sl == 0) {
+    mrow[0] = !((cur == 0) && anyf);
+    cur_out[bb] = cur;
+    used_out[bb] = used;
+    vcap_out[bb] = vcap;
+    done_out[bb] = done;
+    step_reward_out[bb] = 0;
+    reward_out[bb] = -(float)dist;
+    len_out[bb] = len;
+    if (!done) set_status(status, CO_ST_TRUNCATED);
+    atomicMax(tmax, len);
   }
 }
 
@@ -273,9 +329,8 @@ __global__ __launch_bounds__(256) void cvrp_pad_kernel(int64_t B, const int32_t*
   }
 }
 
-inline unsigned group_grid(int64_t B, int G) {
-  const int64_t waves = (B * G + 63) / 64;
-  return grid_for(waves, 4, 256 * 32);
+inline unsigned group_grid(int64_t B, int G) {  // a wave per 64/G instances, covering B
+  return cover_grid((B * G + 63) / 64, 4);
 }
 
 }  // namespace
@@ -287,12 +342,14 @@ int co_internal_tsp_nearest_rollout(int64_t B, int64_t N, const float* locs, int
                                     float* reward_out, void* stream) {
   const float2* l2 = reinterpret_cast<const float2*>(locs);
   hipStream_t s = (hipStream_t)stream;
+  if (group_grid(B, 64) == 0) return CO_E_INVAL;
 #define CO_TSPN(G, EPL)                                                                        \
   hipLaunchKernelGGL((tsp_nearest_episode_kernel<G, EPL>), dim3(group_grid(B, G)), dim3(256),  \
                      0, s, B, (int)N, l2, acts_out, mask_out, first_out, cur_out, i_out,       \
                      done_out, step_reward_out, reward_out)
   if (N <= 32) CO_TSPN(4, 8);
   else if (N <= 64) CO_TSPN(8, 8);
+  else if (N <= 112) CO_TSPN(16, 7);
   else if (N <= 128) CO_TSPN(16, 8);
   else if (N <= 256) CO_TSPN(32, 8);
   else if (N <= 512) CO_TSPN(64, 8);
@@ -308,7 +365,9 @@ extern "C" int co_cvrp_rollout(int64_t B, int64_t N, const float* depot, const f
                                uint8_t* mask_out, uint8_t* done_out, uint8_t* step_reward_out,
                                float* reward_out, int32_t* len_out, int32_t* steps_out,
                                int32_t* status, void* stream) {
-  if (B < 0 || N <= 0 || N > 1023 || max_steps <= 0 || max_steps > (1 << 30)) return CO_E_INVAL;
+  // the episode's step count is packed into 15 bits in the kernel; instance indices are int
+  if (B < 0 || B > 0x7fffffff || N <= 0 || N > 1023 || max_steps <= 0 || max_steps > 0x7fff)
+    return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!depot || !locs || !demand || !acts_out || !cur_out || !used_out || !vcap_out ||
       !visited_out || !mask_out || !done_out || !step_reward_out || !reward_out || !len_out ||
@@ -318,6 +377,7 @@ extern "C" int co_cvrp_rollout(int64_t B, int64_t N, const float* depot, const f
        reinterpret_cast<uintptr_t>(locs_out)) & 7)
     return CO_E_ALIGN;
   hipStream_t s = (hipStream_t)stream;
+  if (group_grid(B, 64) == 0) return CO_E_INVAL;
   if (zero_i32(steps_out, s) != hipSuccess) return launch_status();
   const float2* d2 = reinterpret_cast<const float2*>(depot);
   const float2* l2 = reinterpret_cast<const float2*>(locs);
@@ -330,6 +390,7 @@ extern "C" int co_cvrp_rollout(int64_t B, int64_t N, const float* depot, const f
   const int64_t M = N + 1;
   if (M <= 32) CO_CVRPN(4, 8);
   else if (M <= 64) CO_CVRPN(8, 8);
+  else if (M <= 112) CO_CVRPN(16, 7);
   else if (M <= 128) CO_CVRPN(16, 8);
   else if (M <= 256) CO_CVRPN(32, 8);
   else if (M <= 512) CO_CVRPN(64, 8);

@@ -116,7 +116,74 @@ __global__ __launch_bounds__(256) void pomo_baseline_kernel(int64_t B, int S, co
   }
 }
 
+// The decode loop's epilogue on step-major rows: a 256-thread workgroup owns 64 instances
+// (columns b0 .. b0+63 of the step rows) and walks the steps in chunks of kStackChunk:
+// the chunk's action / log-probability rows are loaded coalesced (a wave reads one step's
+// 64 values) into LDS, then written out transposed -- each instance's chunk of its
+// [B, T] rows as 4 threads x 8 consecutive values -- while thread b sums its row's
+// log-probabilities in step order in f64 (ll) and tests `> -1000` (decoding.py:57-58).
+constexpr int kStackChunk = 32;
+
+__global__ __launch_bounds__(256) void episode_stack_kernel(
+    int64_t B, int64_t T, const int64_t* __restrict__ act_sm, int64_t act_rs,
+    const float* __restrict__ logp_sm, int64_t logp_rs, int64_t* __restrict__ actions,
+    float* __restrict__ logprobs, float* __restrict__ ll, int32_t* status) {
+  __shared__ int64_t s_act[kStackChunk][64];
+  __shared__ float s_lp[kStackChunk][65];  // +1: the row-wise sum reads down a column
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int64_t b0 = (int64_t)blockIdx.x * 64;
+  const int nb = (int)(B - b0 < 64 ? B - b0 : 64);
+  double acc = 0.0;
+  bool bad = false;
+  for (int64_t t0 = 0; t0 < T; t0 += kStackChunk) {
+    const int nt = (int)(T - t0 < kStackChunk ? T - t0 : kStackChunk);
+    for (int k = w; k < nt; k += 4) {  // step t0 + k: one coalesced row piece per wave
+      if (lane < nb) {
+        if (act_sm) s_act[k][lane] = act_sm[(t0 + k) * act_rs + b0 + lane];
+        if (logp_sm) s_lp[k][lane] = logp_sm[(t0 + k) * logp_rs + b0 + lane];
+      }
+    }
+    __syncthreads();
+    // transposed stores: row r = tid / 4, its values j = (tid % 4) * 8 .. + 7 of the chunk
+    const int r = tid >> 2, j0 = (tid & 3) * 8;
+    if (r < nb) {
+      const int64_t ob = (b0 + r) * T + t0;
+#pragma unroll
+      for (int j = j0; j < j0 + 8; ++j) {
+        if (j < nt) {
+          if (actions) actions[ob + j] = s_act[j][r];
+          if (logprobs) logprobs[ob + j] = s_lp[j][r];
+        }
+      }
+    }
+    if (logp_sm && tid < nb) {  // thread b: its row, in step order
+      for (int j = 0; j < nt; ++j) {
+        const float v = s_lp[j][tid];
+        acc += (double)v;
+        bad |= !(v > -1000.f);
+      }
+    }
+    __syncthreads();  // the next chunk overwrites the tile
+  }
+  if (logp_sm && tid < nb && ll) ll[b0 + tid] = (float)acc;
+  if (__any(bad) && lane == 0) set_status(status, CO_ST_LOGP_NEG_INF);
+}
+
 }  // namespace
+
+extern "C" int co_episode_stack(int64_t B, int64_t T, const int64_t* act_sm, int64_t act_rs,
+                                const float* logp_sm, int64_t logp_rs, int64_t* actions,
+                                float* logprobs, float* ll, int32_t* status, void* stream) {
+  if (B < 0 || T < 0 || (act_sm && act_rs < B) || (logp_sm && logp_rs < B)) return CO_E_INVAL;
+  if (B == 0 || T == 0) return CO_OK;
+  if ((act_sm && !actions) || (logp_sm && (!logprobs || !status)) || (ll && !logp_sm))
+    return CO_E_INVAL;
+  const unsigned grid = cover_grid(B, 64);
+  if (grid == 0) return CO_E_INVAL;
+  hipLaunchKernelGGL(episode_stack_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, T,
+                     act_sm, act_rs, logp_sm, logp_rs, actions, logprobs, ll, status);
+  return launch_status();
+}
 
 extern "C" int co_pomo_shared_baseline(int64_t B, int64_t S, const float* reward, const float* ll,
                                        float* bl, float* maxr, int64_t* best, float* adv,

@@ -29,6 +29,8 @@ using SlapDecodeStep = decltype(&co_slap_decode_step);
 using CvrpDecodeStep = decltype(&co_cvrp_decode_step);
 using DecodeStep = decltype(&co_decode_step);
 using CvrpStep = decltype(&co_cvrp_step);
+using SlapReset = decltype(&co_slap_reset);
+using EpisodeStack = decltype(&co_episode_stack);
 
 inline bool is_tensor(PyObject* o) { return o != Py_None && THPVariable_Check(o); }
 
@@ -137,15 +139,22 @@ struct StatePool {
   void clear() { entries.clear(); }
 };
 
+// The per-step [B] action and log-probability of consecutive steps are consecutive rows
+// of one storage: step k takes [action row | log-probability row], so the rows of an
+// episode form two step-major slabs with a uniform row stride, which the epilogue
+// (episode_stack -> co_episode_stack) transposes in one launch instead of two
+// torch.stack calls.  slab_fresh(steps) makes the next take start a new storage sized for
+// an episode of that many steps, so an episode does not straddle two storages.
 struct Slab {
   static constexpr int64_t kSteps = 64;
   c10::Device dev{c10::DeviceType::CPU};
   c10::Storage st;
-  int64_t off = 0, cap = 0;
+  int64_t off = 0, cap = 0, fresh_steps = 0;
   // a region of nbytes (a multiple of kAlign): offset into `st`
   int64_t take(const c10::Device& d, int64_t nbytes) {
-    if (!st || d != dev || off + nbytes > cap) {
-      cap = nbytes * kSteps;
+    if (!st || d != dev || off + nbytes > cap || fresh_steps > 0) {
+      cap = nbytes * (fresh_steps > 0 ? fresh_steps : kSteps);
+      fresh_steps = 0;
       st = new_storage(d, cap);
       dev = d;
       off = 0;
@@ -257,6 +266,7 @@ PyObject* tsp_decode_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
 // A record (version, value) in a tensor's attribute: valid while the tensor's version
 // counter is unchanged (nobody modified it in place since the env produced it).
 PyObject* g_attr_i = nullptr;  // "_co_i": the value every entry of an `i` tensor holds
+PyObject* g_attr_tc = nullptr;  // "_co_tc": to_choose is the env's untouched arange from k on
 
 // the record's value, or -1 (absent / stale)
 long long known(PyObject* t, PyObject* attr) {
@@ -402,12 +412,27 @@ inline PyObject* td_tensor(PyObject* td, const char* k) {  // borrowed; nullptr 
   return (o && is_tensor(o)) ? o : nullptr;
 }
 
+// True when `o` (a tensor the td dict holds) is referenced by nothing but that dict: one
+// Python reference, one at::Tensor handle, a storage of its own (no views, no pool), no
+// autograd.  Writing it in place then cannot be told apart from writing a fresh copy.
+inline bool exclusively_held(PyObject* o, const at::Tensor& t) {
+  return Py_REFCNT(o) == 1 && t.use_count() == 1 && t.storage().use_count() == 1 &&
+         !t.requires_grad() && t.is_contiguous() && t.storage_offset() == 0;
+}
+
 // slap_step_td(fn, lb_attr, td, logits, mode, temp, clip, action_in, seed, offset, status,
 //              key) -> (action, logp) | None | error code
 // SLAPEnv.decode_and_step (envs/slap.py) on a dict-backed TensorDict in one call: reads
 // action_mask / i / to_choose / assignment / freq, launches co_slap_decode_step into fresh
 // outputs, stores assignment / to_choose[:, 1:] / action_mask / i / reward / done and the
-// action, records the done lower bound on the new i.
+// action, records the done lower bound on the new i.  Two traffic savings, both invisible
+// to the caller:
+// * to_choose that is still the env's untouched arange (record "_co_tc" = k, version
+//   unchanged) is not read: the kernel takes the uniform product k (co_env.h);
+// * the assignment is the reference's clone with one element changed (slap/env.py:50-54):
+//   when nothing but the td refers to the input assignment, that element is written in
+//   place; otherwise the row is copied into a new storage of its own (so the next step can
+//   write it in place).
 PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (n != 12) {
     PyErr_SetString(PyExc_TypeError, "slap_step_td: 12 arguments");
@@ -426,6 +451,7 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (!mask_o || !i_o || !tc_o || !as_o || !fr_o) Py_RETURN_NONE;
   const auto fn = fn_at<SlapDecodeStep>(a[0]);
   const long long ki = known(i_o, g_attr_i);
+  const long long ktc = known(tc_o, g_attr_tc);
   const long mode = PyLong_AsLong(a[4]);
   const double temp = PyFloat_AsDouble(a[5]), clip = PyFloat_AsDouble(a[6]);
   const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[8]);
@@ -456,16 +482,19 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
         asg.size(0) != b)
       Py_RETURN_NONE;
     if (ain && !fits(*ain, dev, at::kLong, b)) Py_RETURN_NONE;
+    // the untouched arange: to_choose[:, 0] == k in every row (k + remaining columns == P)
+    const bool uniform = ktc >= 0 && ktc < p && ktc + tc.size(1) == p;
+    const bool in_place = exclusively_held(as_o, asg);
     const int64_t kb = up(8 * b);
     const int64_t ko = g_slab.take(dev, 2 * kb);
     at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
     at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b});
     Carver c;
-    const int64_t oa = c.take(4 * b * p), om = c.take(b * l), oi = c.take(8 * b), od = c.take(b),
-                  orw = c.take(b);
+    const int64_t om = c.take(b * l), oi = c.take(8 * b), od = c.take(b), orw = c.take(b);
     void* stream = current_stream(dev);
     const c10::Storage st = g_state.acquire(dev, c.off, stream);
-    at::Tensor asg_out = view_of(st, at::kInt, oa, asg.sizes());
+    at::Tensor asg_out = in_place ? asg : view_of(new_storage(dev, 4 * b * p), at::kInt, 0,
+                                                  asg.sizes());
     at::Tensor mask_out = view_of(st, at::kBool, om, {b, l});
     at::Tensor i_out = view_of(st, at::kLong, oi, i.sizes());
     at::Tensor done = view_of(st, at::kBool, od, {b, 1});
@@ -475,7 +504,8 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     rc = fn(b, l, p, logits.const_data_ptr<float>(), logits.stride(0),
             static_cast<const uint8_t*>(mask.const_data_ptr()), (float)clip, (float)temp, (int)mode,
             ain ? ain->const_data_ptr<int64_t>() : nullptr, act.mutable_data_ptr<int64_t>(),
-            logp.mutable_data_ptr<float>(), seed, offset, tc.const_data_ptr<float>(), tc.stride(0),
+            logp.mutable_data_ptr<float>(), seed, offset,
+            uniform ? nullptr : tc.const_data_ptr<float>(), uniform ? ktc : tc.stride(0),
             asg.const_data_ptr<int32_t>(), asg_out.mutable_data_ptr<int32_t>(),
             static_cast<uint8_t*>(mask_out.mutable_data_ptr()), i.const_data_ptr<int64_t>(),
             i_out.mutable_data_ptr<int64_t>(), static_cast<uint8_t*>(done.mutable_data_ptr()),
@@ -483,8 +513,13 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
             status.mutable_data_ptr<int32_t>(), stream);
     Py_END_ALLOW_THREADS
     if (rc != CO_OK) return PyLong_FromLong(rc);
+    if (in_place) asg.unsafeGetTensorImpl()->bump_version();  // an in-place write
     PyObject* tc_next = THPVariable_Wrap(tc.slice(1, 1));  // to_choose[:, 1:] (a view)
     if (!tc_next) return nullptr;
+    if (uniform && remember(tc_next, g_attr_tc, ktc + 1)) {
+      Py_DECREF(tc_next);
+      return nullptr;
+    }
     PyObject* res = td_finish(td, key, ain_o, act, logp,
                               {{"assignment", &asg_out}, {"action_mask", &mask_out},
                                {"i", &i_out}, {"reward", &reward}, {"done", &done}},
@@ -714,6 +749,168 @@ PyObject* cvrp_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
   }
 }
 
+// slab_fresh(steps) -> None: the next step's action / log-probability rows start a new
+// slab storage sized for `steps` steps (DecodingStrategy calls it at an episode's first
+// step with the env's bound on the episode length)
+PyObject* slab_fresh(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 1) {
+    PyErr_SetString(PyExc_TypeError, "slab_fresh: 1 argument");
+    return nullptr;
+  }
+  const long long steps = PyLong_AsLongLong(a[0]);
+  if (PyErr_Occurred()) return nullptr;
+  g_slab.fresh_steps = steps < 1 ? 1 : (steps > 4096 ? 4096 : steps);
+  Py_RETURN_NONE;
+}
+
+// episode_stack(fn, actions, logprobs, status, want_ll) -> (actions[B,T], logprobs[B,T],
+//   ll[B] | None) | None | error code
+// DecodingStrategy.post_decoder_hook's torch.stack(self.actions, 1) / torch.stack(
+// self.logprobs, 1), get_log_likelihood's sum and its `> -1000` test (CO_ST_LOGP_NEG_INF in
+// status) as one co_episode_stack launch -- when the two lists hold [B] tensors that are
+// consecutive rows of step-major slabs (what the step calls above return); None otherwise
+// (the caller stacks as before).
+PyObject* episode_stack(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 5) {
+    PyErr_SetString(PyExc_TypeError, "episode_stack: 5 arguments");
+    return nullptr;
+  }
+  PyObject *al = a[1], *ll_ = a[2];
+  if (!PyList_Check(al) || !PyList_Check(ll_) || !is_tensor(a[3])) Py_RETURN_NONE;
+  const Py_ssize_t T = PyList_GET_SIZE(al);
+  if (T < 1 || PyList_GET_SIZE(ll_) != T) Py_RETURN_NONE;
+  const auto fn = fn_at<EpisodeStack>(a[0]);
+  const int want_ll = PyObject_IsTrue(a[4]);
+  if (want_ll < 0) return nullptr;
+  try {
+    const at::Tensor& status = THPVariable_Unpack(a[3]);
+    // the rows: [B] tensors, one storage per list, a uniform stride between steps
+    int64_t b = -1, rs[2] = {0, 0};
+    const void* base[2] = {nullptr, nullptr};
+    c10::Device dev{c10::DeviceType::CPU};
+    for (int li = 0; li < 2; ++li) {
+      PyObject* lst = li == 0 ? al : ll_;
+      const at::ScalarType dt = li == 0 ? at::kLong : at::kFloat;
+      const int64_t esz = li == 0 ? 8 : 4;
+      const c10::StorageImpl* sti = nullptr;
+      for (Py_ssize_t t = 0; t < T; ++t) {
+        PyObject* o = PyList_GET_ITEM(lst, t);
+        if (!is_tensor(o)) Py_RETURN_NONE;
+        const at::Tensor& x = THPVariable_Unpack(o);
+        if (x.dim() != 1 || x.scalar_type() != dt || x.stride(0) != 1 || x.requires_grad())
+          Py_RETURN_NONE;
+        if (t == 0 && li == 0) {
+          dev = x.device();
+          b = x.size(0);
+          if (!dev.is_cuda() || b < 1) Py_RETURN_NONE;
+        }
+        if (x.device() != dev || x.size(0) != b) Py_RETURN_NONE;
+        const char* p = static_cast<const char*>(x.const_data_ptr());
+        if (t == 0) {
+          base[li] = p;
+          sti = x.storage().unsafeGetStorageImpl();
+        } else {
+          if (x.storage().unsafeGetStorageImpl() != sti) Py_RETURN_NONE;
+          const int64_t d = p - static_cast<const char*>(base[li]);
+          if (t == 1) {
+            if (d <= 0 || d % esz != 0 || d / esz < b) Py_RETURN_NONE;
+            rs[li] = d / esz;
+          } else if (d != (int64_t)t * rs[li] * esz) {
+            Py_RETURN_NONE;
+          }
+        }
+      }
+      if (T == 1) rs[li] = b;
+    }
+    if (status.device() != dev || status.scalar_type() != at::kInt) Py_RETURN_NONE;
+    const auto o64 = at::TensorOptions().device(dev).dtype(at::kLong);
+    const auto o32 = at::TensorOptions().device(dev).dtype(at::kFloat);
+    at::Tensor acts = at::empty({b, (int64_t)T}, o64);
+    at::Tensor lps = at::empty({b, (int64_t)T}, o32);
+    at::Tensor ll;
+    if (want_ll) ll = at::empty({b}, o32);
+    void* stream = current_stream(dev);
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = fn(b, (int64_t)T, static_cast<const int64_t*>(base[0]), rs[0],
+            static_cast<const float*>(base[1]), rs[1], acts.mutable_data_ptr<int64_t>(),
+            lps.mutable_data_ptr<float>(), want_ll ? ll.mutable_data_ptr<float>() : nullptr,
+            status.mutable_data_ptr<int32_t>(), stream);
+    Py_END_ALLOW_THREADS
+    if (rc != CO_OK) return PyLong_FromLong(rc);
+    return wrap_all({&acts, &lps, &ll});
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
+// slap_reset_td(fn, lb_attr, td) -> True | None | error code
+// SLAPEnv._reset (slap/env.py:95-129) + RL4COEnvBase.reset's done / terminated zeros on a
+// dict-backed TensorDict in one co_slap_reset launch: mask / to_choose / i / reward /
+// ratio / done / terminated carved from one storage and stored in the td; records i = 0,
+// the done lower bound P, and the untouched-arange record of to_choose (offset 0).
+PyObject* slap_reset_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 3) {
+    PyErr_SetString(PyExc_TypeError, "slap_reset_td: 3 arguments");
+    return nullptr;
+  }
+  PyObject *lb_attr = a[1], *td = a[2];
+  if (!PyDict_Check(td) || !PyUnicode_Check(lb_attr)) Py_RETURN_NONE;
+  PyObject *as_o = td_tensor(td, "assignment"), *fr_o = td_tensor(td, "freq"),
+           *lo_o = td_tensor(td, "locs"), *dd_o = td_tensor(td, "depot_loc_dist");
+  if (!as_o || !fr_o || !lo_o || !dd_o) Py_RETURN_NONE;
+  const auto fn = fn_at<SlapReset>(a[0]);
+  try {
+    const at::Tensor& asg = THPVariable_Unpack(as_o);
+    const at::Tensor& fr = THPVariable_Unpack(fr_o);
+    const at::Tensor& lo = THPVariable_Unpack(lo_o);
+    const at::Tensor& dd = THPVariable_Unpack(dd_o);
+    const c10::Device dev = asg.device();
+    if (!dev.is_cuda() || asg.dim() < 1 || fr.dim() < 2 || lo.dim() < 2 || dd.dim() != 2)
+      Py_RETURN_NONE;
+    const int64_t b = asg.size(0), p = fr.size(fr.dim() - 2), l = lo.size(1);
+    if (dd.size(0) != b || dd.size(1) != l) Py_RETURN_NONE;
+    Carver c;
+    const int64_t om = c.take(b * l), ot = c.take(4 * b * p), oi = c.take(8 * b),
+                  orw = c.take(4 * b), ora = c.take(4 * b * l), od = c.take(b), oe = c.take(b);
+    c10::Storage st = new_storage(dev, c.off);
+    at::Tensor mask = view_of(st, at::kBool, om, {b, l});
+    at::Tensor tc = view_of(st, at::kFloat, ot, {b, p});
+    at::Tensor it = view_of(st, at::kLong, oi, {b, 1});
+    at::Tensor rw = view_of(st, at::kFloat, orw, {b, 1});
+    at::Tensor ratio = view_of(st, at::kFloat, ora, {b, l});
+    at::Tensor done = view_of(st, at::kBool, od, {b, 1});
+    at::Tensor term = view_of(st, at::kBool, oe, {b, 1});
+    void* stream = current_stream(dev);
+    int rc;
+    Py_BEGIN_ALLOW_THREADS
+    rc = fn(b, l, p, static_cast<uint8_t*>(mask.mutable_data_ptr()), tc.mutable_data_ptr<float>(),
+            it.mutable_data_ptr<int64_t>(), rw.mutable_data_ptr<float>(),
+            ratio.mutable_data_ptr<float>(), static_cast<uint8_t*>(done.mutable_data_ptr()),
+            static_cast<uint8_t*>(term.mutable_data_ptr()), stream);
+    Py_END_ALLOW_THREADS
+    if (rc != CO_OK) return PyLong_FromLong(rc);
+    std::pair<const char*, at::Tensor*> outs[] = {
+        {"to_choose", &tc}, {"i", &it},       {"ratio", &ratio},   {"action_mask", &mask},
+        {"reward", &rw},    {"done", &done}, {"terminated", &term}};
+    for (auto& kv : outs) {
+      PyObject* o = THPVariable_Wrap(std::move(*kv.second));
+      if (!o) return nullptr;
+      int err = 0;
+      if (kv.first[0] == 'i') err = remember(o, g_attr_i, 0) || remember(o, lb_attr, p);
+      else if (kv.first[0] == 't' && kv.first[1] == 'o') err = remember(o, g_attr_tc, 0);
+      if (!err) err = PyDict_SetItemString(td, kv.first, o);
+      Py_DECREF(o);
+      if (err) return nullptr;
+    }
+    Py_RETURN_TRUE;
+  } catch (const std::exception& e) {
+    PyErr_SetString(PyExc_RuntimeError, e.what());
+    return nullptr;
+  }
+}
+
 // clear_pool() -> None: drop every pooled state storage (tensors still held stay valid)
 PyObject* clear_pool(PyObject*, PyObject* const*, Py_ssize_t) {
   g_state.clear();
@@ -727,6 +924,14 @@ PyMethodDef methods[] = {
      METH_FASTCALL, "CVRPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
     {"clear_pool", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(clear_pool)),
      METH_FASTCALL, "drop the pooled step-state storages"},
+    {"slab_fresh", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(slab_fresh)),
+     METH_FASTCALL, "start a new action / log-probability slab at the next step"},
+    {"episode_stack",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(episode_stack)),
+     METH_FASTCALL, "the decode loop's stack + log-likelihood epilogue in one launch"},
+    {"slap_reset_td",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(slap_reset_td)),
+     METH_FASTCALL, "SLAPEnv._reset + the reset's done / terminated in one launch"},
     {"tsp_step_td", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(tsp_step_td)),
      METH_FASTCALL, "TSPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
     {"decode_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(decode_step)),
@@ -745,6 +950,7 @@ PyModuleDef module = {PyModuleDef_HEAD_INIT, "_co_torchstep",
 
 PyMODINIT_FUNC PyInit__co_torchstep(void) {
   g_attr_i = PyUnicode_InternFromString("_co_i");
-  if (!g_attr_i) return nullptr;
+  g_attr_tc = PyUnicode_InternFromString("_co_tc");
+  if (!g_attr_i || !g_attr_tc) return nullptr;
   return PyModule_Create(&module);
 }

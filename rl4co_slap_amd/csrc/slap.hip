@@ -24,7 +24,8 @@ namespace {
 __global__ __launch_bounds__(256) void slap_reset_kernel(int64_t B, int64_t L, int64_t P,
                                                          uint8_t* mask, float* to_choose,
                                                          int64_t* it, float* reward,
-                                                         float* ratio) {
+                                                         float* ratio, uint8_t* done,
+                                                         uint8_t* terminated) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // 16-byte units where the buffers allow it (the launcher checks alignment)
@@ -55,6 +56,8 @@ __global__ __launch_bounds__(256) void slap_reset_kernel(int64_t B, int64_t L, i
   for (int64_t b = t0; b < B; b += stride) {
     it[b] = 0;
     reward[b] = 0.f;
+    if (done) done[b] = 0;
+    if (terminated) terminated[b] = 0;
   }
 }
 
@@ -72,7 +75,10 @@ struct SlapRowEpilogue {
     int64_t i;
     float product;
   };
-  __device__ Row load(int64_t b) const { return {i_in[b], to_choose[b * tc_stride]}; }
+  // to_choose NULL: every row's product is tc_stride (the untouched arange at that step)
+  __device__ Row load(int64_t b) const {
+    return {i_in[b], to_choose ? to_choose[b * tc_stride] : (float)tc_stride};
+  }
   __device__ void store(int64_t b, int64_t action, int, const Row& r) const {
     int64_t p = (int64_t)(int)r.product;  // .to(torch.int), env.py:52
     if (p < 0) p += P;
@@ -419,7 +425,8 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
   }
   int64_t it = 0;
   if (sl == 0) it = i_in[bb];
-  const float prod = to_choose[bb * tc_stride];  // every lane (one broadcast line)
+  // every lane (one broadcast line); to_choose NULL: the uniform product tc_stride
+  const float prod = to_choose ? to_choose[bb * tc_stride] : (float)tc_stride;
   int bi = 0x7fffffff;
   int64_t a_raw = 0;
   if constexpr (CLOSEST) {
@@ -482,12 +489,14 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
 }  // namespace
 
 extern "C" int co_slap_reset(int64_t B, int64_t L, int64_t P, uint8_t* mask, float* to_choose,
-                             int64_t* it, float* reward, float* ratio, void* stream) {
+                             int64_t* it, float* reward, float* ratio, uint8_t* done,
+                             uint8_t* terminated, void* stream) {
   if (B < 0 || L <= 0 || P <= 0) return CO_E_INVAL;
   if (B == 0) return CO_OK;
   if (!mask || !to_choose || !it || !reward) return CO_E_INVAL;
   hipLaunchKernelGGL(slap_reset_kernel, dim3(grid_for(B * L / 16 + 1, 256)), dim3(256), 0,
-                     (hipStream_t)stream, B, L, P, mask, to_choose, it, reward, ratio);
+                     (hipStream_t)stream, B, L, P, mask, to_choose, it, reward, ratio, done,
+                     terminated);
   return launch_status();
 }
 
@@ -498,8 +507,8 @@ extern "C" int co_slap_step(int64_t B, int64_t L, int64_t P, const int64_t* acti
                             int32_t* status, void* stream) {
   if (B < 0 || L <= 0 || P <= 0 || L > (1 << 30)) return CO_E_INVAL;
   if (B == 0) return CO_OK;
-  if (!action || !to_choose || !assign_in || !assign_out || !mask_in || !mask_out || !i_in ||
-      !i_out || !done || !reward)
+  if (!action || !assign_in || !assign_out || !mask_in || !mask_out || !i_in || !i_out || !done ||
+      !reward || (!to_choose && (tc_stride < 0 || tc_stride >= P)))
     return CO_E_INVAL;
   // 16 lanes per instance (the closest-step layout without the policy) for L % 4 == 0,
   // L <= 256 and 4-B-aligned mask rows; else the 64-row byte tile
@@ -599,8 +608,8 @@ extern "C" int co_slap_closest_step(int64_t B, int64_t L, int64_t P, const float
                                     uint8_t* reward, int32_t* status, void* stream) {
   if (B < 0 || L <= 0 || P <= 0 || L > (1 << 30)) return CO_E_INVAL;
   if (B == 0) return CO_OK;
-  if (!dist || !to_choose || !assign_in || !assign || !mask_in || !mask_out || !action_out || !i_in || !i_out ||
-      !done || !reward)
+  if (!dist || !assign_in || !assign || !mask_in || !mask_out || !action_out || !i_in || !i_out ||
+      !done || !reward || (!to_choose && (tc_stride < 0 || tc_stride >= P)))
     return CO_E_INVAL;
   const bool vec = L % 4 == 0 && L <= 4 * 16 * 4 &&
                    ((reinterpret_cast<uintptr_t>(dist) & 15) |

@@ -101,10 +101,13 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         if td.device is None or td.device != self.device:
             td = td.to(self.device)
         out = self._reset(td, batch_size=batch_size)
+        if out is td:  # the env stored its reset state, done / terminated included, in td
+            return td
         td.update(out)
-        z = torch.zeros((*batch_size, 1), dtype=torch.bool, device=self.device)
-        td.set("done", z)
-        td.set("terminated", torch.zeros_like(z))
+        if "done" not in out:  # else the env's reset kernel wrote the zeros
+            z = torch.zeros((2, *batch_size, 1), dtype=torch.bool, device=self.device)
+            td.set("done", z[0])
+            td.set("terminated", z[1])
         return td
 
     @abc.abstractmethod
@@ -186,17 +189,32 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
         return self
 
     # -- status word -------------------------------------------------------------
-    @staticmethod
-    def raise_for_status(status: torch.Tensor, messages):
+    # While a decode loop collects its checks (``DecodingStrategy.defer_checks``), the
+    # reward's status word is a word of the strategy's status tensor and its read is
+    # deferred to the loop's single host read (``_checks``: the collector).
+    _checks = None
+
+    def status_word(self, device) -> torch.Tensor:
+        """A zeroed status word for one of this env's kernels."""
+        if self._checks is not None:
+            return self._checks.env_word()
+        return nat.scratch_status(device)
+
+    def raise_for_status(self, status: torch.Tensor, messages):
         """Read a device status word (one host sync, which also carries the device's
         deferred word: an earlier out-of-range ``gather_by_index``) and raise the
-        reference's error."""
+        reference's error -- or, inside a decode loop's collection, register the messages
+        for its single read."""
+        if self._checks is not None and self._checks.owns(status):
+            self._checks.add(messages)
+            return
         d = nat.pending_deferred(status.device) if status.device.type != "cpu" else None
         if d is not None:
             bits, dbits = (int(v) for v in torch.cat([status.reshape(1), d]).tolist())
             nat.raise_deferred(dbits, status.device)
         else:
             bits = int(status.item())
+        nat.release_status(status, (bits,))
         for bit, exc, msg in messages:
             if bits & bit:
                 raise exc(msg)

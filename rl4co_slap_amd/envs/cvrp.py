@@ -252,7 +252,7 @@ class CVRPEnv(RL4COEnvBase):
         b, t = actions.shape
         n = demand.shape[-1]
         reward = torch.empty(b, dtype=torch.float32, device=locs.device)
-        status = nat.scratch_status(locs.device)
+        status = self.status_word(locs.device)
         nat.call("co_cvrp_reward", b, n, t, nat.ptr(locs), nat.ptr(actions), actions.stride(0),
                  actions.stride(1), nat.ptr(demand), nat.ptr(vcap), int(check), nat.ptr(reward),
                  nat.ptr(status), nat.stream_of(locs))

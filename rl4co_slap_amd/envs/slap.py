@@ -116,7 +116,17 @@ class SLAPEnv(RL4COEnvBase):
         self.check_solution = check_solution
 
     def _reset(self, td=None, batch_size=None) -> TensorDict:
-        """``slap/env.py:95-129`` in one kernel (``to_choose``/``ratio`` on the device)."""
+        """``slap/env.py:95-129`` in one kernel (``to_choose``/``ratio`` on the device),
+        which also writes the ``done`` / ``terminated`` zeros ``reset`` adds.  On a device
+        stand-in TensorDict the step glue does it in one call (one storage for the seven
+        outputs, set straight into ``td``)."""
+        ts = nat.torchstep() if type(td) is TensorDict else None
+        if ts is not None:
+            r = ts.slap_reset_td(self._lb_attr, td)
+            if type(r) is int:
+                nat.check_rc("co_slap_reset", r)
+            if r is not None:
+                return td
         assignment = td["assignment"]
         nat.require_device(assignment)
         b = assignment.shape[0]
@@ -128,13 +138,15 @@ class SLAPEnv(RL4COEnvBase):
         i = torch.empty((b, 1), dtype=torch.int64, device=dev)
         reward = torch.empty((b, 1), dtype=torch.float32, device=dev)
         ratio = torch.empty(td["depot_loc_dist"].shape, dtype=torch.float32, device=dev)
+        dt = torch.empty((2, b, 1), dtype=torch.bool, device=dev)  # done, terminated
         nat.call("co_slap_reset", b, l, p, nat.ptr(mask), nat.ptr(to_choose), nat.ptr(i),
-                 nat.ptr(reward), nat.ptr(ratio), nat.stream_of(assignment))
+                 nat.ptr(reward), nat.ptr(ratio), nat.ptr(dt[0]), nat.ptr(dt[1]),
+                 nat.stream_of(assignment))
         self._remember_lb(i, p)  # done = (i == P-1) before the step (slap/env.py:57)
         self._remember_i(i, 0)
         return TensorDict({"assignment": assignment, "to_choose": to_choose, "i": i,
-                           "ratio": ratio, "action_mask": mask, "reward": reward},
-                          batch_size=batch_size)
+                           "ratio": ratio, "action_mask": mask, "reward": reward,
+                           "done": dt[0], "terminated": dt[1]}, batch_size=batch_size)
 
     def _step(self, td: TensorDict) -> TensorDict:
         """``slap/env.py:38-93``: one kernel replaces the clone + advanced-index write +
@@ -254,7 +266,7 @@ class SLAPEnv(RL4COEnvBase):
         assign, picklist, locs = assign.contiguous(), picklist.contiguous(), locs.contiguous()
         b, o, k = picklist.shape
         reward = torch.empty(b, dtype=torch.float32, device=locs.device)
-        status = nat.scratch_status(locs.device)
+        status = self.status_word(locs.device)
         nat.call("co_slap_reward", b, locs.shape[1], assign.shape[1], o, k, nat.ptr(assign),
                  nat.ptr(picklist), nat.ptr(locs), nat.ptr(reward), nat.ptr(status),
                  nat.stream_of(locs))

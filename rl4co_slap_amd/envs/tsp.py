@@ -203,7 +203,7 @@ class TSPEnv(RL4COEnvBase):
             actions = actions.long()
         b, t = actions.shape
         reward = torch.empty(b, dtype=torch.float32, device=locs.device)
-        status = nat.scratch_status(locs.device)
+        status = self.status_word(locs.device)
         nat.call("co_tsp_reward", b, locs.shape[-2], t, nat.ptr(locs), locs.shape[0],
                  nat.ptr(actions),
                  actions.stride(0), actions.stride(1), int(check), nat.ptr(reward),

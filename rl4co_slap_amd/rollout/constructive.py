@@ -22,7 +22,7 @@ from torch import nn
 
 from ..envs import get_env
 from ..envs.base import RL4COEnvBase
-from ..utils.decoding import get_decoding_strategy, get_log_likelihood
+from ..utils.decoding import DecodingStrategy, get_decoding_strategy, get_log_likelihood
 from ..utils.ops import calculate_entropy
 
 log = logging.getLogger(__name__)
@@ -124,6 +124,7 @@ class ConstructivePolicy(nn.Module):
         lb = env.min_steps_to_done(td) if hasattr(env, "min_steps_to_done") else 0
         td, env, num_starts = strategy.pre_decoder_hook(td, env)
         lb -= len(strategy.actions)  # the multistart hook's first step
+        strategy.steps_hint = lb
         hook = getattr(self.decoder, "pre_decoder_hook", None)
         if hook is not None:
             td, env, hidden = hook(td, env, hidden, num_starts)
@@ -149,8 +150,25 @@ class ConstructivePolicy(nn.Module):
             if step > max_steps:
                 log.error(f"Exceeded maximum number of steps ({max_steps}) duing decoding")
                 break
-        logprobs, actions, td, env = strategy.post_decoder_hook(td, env)
-        if calc_reward:
+        # the epilogue (stack + log-likelihood in one launch where it applies), then the
+        # reward, then ONE host read for the decode step's and the reward's checks
+        if type(strategy).post_decoder_hook is DecodingStrategy.post_decoder_hook:
+            logprobs, actions, td, env = strategy._post(td, env, collect=True)
+        else:  # a strategy with its own hook (beam search)
+            logprobs, actions, td, env = strategy.post_decoder_hook(td, env)
+        if getattr(strategy, "checks", None) is not None:
+            env._checks = strategy.checks
+            try:
+                reward = env.get_reward(td, actions) if calc_reward else None
+            except BaseException:
+                env._checks = None
+                strategy.read_checks(logprobs)  # a decode-step error came first
+                raise
+            env._checks = None
+            strategy.read_checks(logprobs)
+            if calc_reward:
+                td.set("reward", reward)
+        elif calc_reward:
             td.set("reward", env.get_reward(td, actions))
         out = {"reward": td["reward"],
                "log_likelihood": get_log_likelihood(logprobs, actions, td.get("mask", None),

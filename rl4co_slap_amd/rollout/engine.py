@@ -140,7 +140,8 @@ class SLAPStepwiseEpisode(_GraphEpisode):
     def _launch(self, s):
         b, l, p = self.b, self.l, self.p
         nat.call("co_slap_reset", b, l, p, nat.ptr(self.mask[0]), nat.ptr(self.to_choose),
-                 nat.ptr(self.i[0]), nat.ptr(self.reset_reward), nat.ptr(self.ratio), s)
+                 nat.ptr(self.i[0]), nat.ptr(self.reset_reward), nat.ptr(self.ratio), None, None,
+                 s)
         for t in range(p):
             src, dst = t & 1, (t + 1) & 1
             a = self.acts[t]

@@ -108,10 +108,12 @@ def process_logits(logits, mask=None, temperature: float = 1.0, top_p: float = 0
 def get_log_likelihood(logprobs, actions=None, mask=None, return_sum: bool = True):
     """``decoding.py:39-65``.  The ``> -1000`` assert needs a host sync; for logprobs
     that ``post_decoder_hook`` produced, the same test was folded into its single
-    status read (``_co_logp_ok``), so no second sync happens here."""
+    status read (``_co_logp_ok``), so no second sync happens here; and when its epilogue
+    kernel (``co_episode_stack``) also summed them, that sum is returned (``_co_ll``)."""
     rec = getattr(logprobs, "_co_logp_ok", None)
     # the folded test is valid only while the tensor is unchanged since it was made
     checked = rec[0] if rec is not None and rec[1] == logprobs._version else None
+    ll = getattr(logprobs, "_co_ll", None) if return_sum and mask is None else None
     if actions is not None and logprobs.dim() == 3:
         logprobs = logprobs.gather(-1, actions.unsqueeze(-1)).squeeze(-1)
     if mask is not None:
@@ -120,6 +122,8 @@ def get_log_likelihood(logprobs, actions=None, mask=None, return_sum: bool = Tru
     if checked is None:
         checked = bool((logprobs > -1000).data.all())
     assert checked, "Logprobs should not be -inf, check sampling procedure!"
+    if ll is not None and ll[1] == logprobs._version:
+        return ll[0]
     return logprobs.sum(1) if return_sum else logprobs
 
 
@@ -166,6 +170,73 @@ def rollout(env, td, policy, max_steps: int = None):
             break
     acts = torch.stack(actions, dim=1)
     return env.get_reward(td, acts), td, acts
+
+
+def _stack_device(actions, logprobs, status):
+    """``torch.stack(actions, 1)`` / ``torch.stack(logprobs, 1)`` + the log-likelihood
+    sum and the ``> -1000`` test through ``co_episode_stack`` on step-major stacks (the
+    same kernel, so the same bits, as the step glue's slab path); None when the per-step
+    tensors are not [B] int64 / f32 device tensors of one device."""
+    a0, l0 = actions[0], logprobs[0]
+    if (a0.dim() != 1 or l0.dim() != 1 or a0.dtype != torch.int64 or l0.dtype != torch.float32
+            or a0.device != status.device or l0.device != status.device):
+        return None
+    A = torch.stack(actions, 0)  # [T, B]: rows are the steps' tensors (checks shapes too)
+    L = torch.stack(logprobs, 0)
+    if A.shape != L.shape or A.dtype != torch.int64 or L.dtype != torch.float32:
+        return None
+    t, b = A.shape
+    acts = torch.empty((b, t), dtype=torch.int64, device=A.device)
+    lps = torch.empty((b, t), dtype=torch.float32, device=A.device)
+    ll = torch.empty(b, dtype=torch.float32, device=A.device)
+    nat.call("co_episode_stack", b, t, nat.ptr(A), b, nat.ptr(L), b, nat.ptr(acts),
+             nat.ptr(lps), nat.ptr(ll), nat.ptr(status), nat.stream_of(A))
+    return acts, lps, ll
+
+
+class _Checks:
+    """The data-dependent checks of one decode episode, read in ONE host sync.
+
+    Word 0 of the strategy's status tensor collects the decode steps' bits (infeasible
+    selection, ``decoding.py:376-379,393-395``; out-of-range env indices) and the
+    epilogue's ``> -1000`` test (``co_episode_stack``, ``decoding.py:57-58``); word 1 is
+    the status word of the kernels an env runs while the collection is open (the reward
+    and its validity asserts, ``base.py:182-188``).  ``read`` raises in the reference's
+    order: the decode step's assertion, then the reward's, and records the
+    log-probability test for ``get_log_likelihood`` (which raises it there)."""
+
+    def __init__(self, status: torch.Tensor):
+        self.status = status
+        self._word1 = None
+        self.env_msgs = []
+
+    def env_word(self) -> torch.Tensor:
+        if self._word1 is None:
+            self._word1 = self.status[1:]
+        return self._word1
+
+    def owns(self, t) -> bool:
+        return self._word1 is not None and t is self._word1
+
+    def add(self, messages):
+        self.env_msgs.extend(messages)
+
+    def read(self):
+        """-> the decode word's bits (the caller raises / records them); raises the env
+        messages and the device's deferred gather errors."""
+        st = self.status
+        d = nat.pending_deferred(st.device) if st.device.type != "cpu" else None
+        vals = [int(v) for v in (torch.cat([st, d]) if d is not None else st).tolist()]
+        if d is not None:
+            nat.raise_deferred(vals[2], st.device)
+        w0, w1 = vals[0], vals[1]
+        if w0 & nat.ST_INFEASIBLE:
+            raise AssertionError("infeasible action selected")
+        for bit, exc, msg in self.env_msgs:
+            if w1 & bit:
+                raise exc(msg)
+        nat.release_status(st, vals[:2])
+        return w0
 
 
 class DecodingStrategy(metaclass=abc.ABCMeta):
@@ -221,8 +292,43 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
 
     def post_decoder_hook(self, td, env):
         """``decoding.py:315-325`` + the deferred feasibility assertion."""
+        out = self._post(td, env, collect=False)
+        return out
+
+    def _post(self, td, env, collect: bool):
+        """``post_decoder_hook``'s work.  On the device, per-step [B] actions (int64) and
+        log-probabilities (f32) are stacked by ONE ``co_episode_stack`` launch that also
+        sums the log-likelihood (``get_log_likelihood``) and tests ``> -1000`` into the
+        status word -- straight from the step glue's slabs when the rows are one block
+        (no torch.stack at all), else from a step-major torch.stack.  collect=True (the
+        decode loop, which reads its checks once after the reward): the status read is
+        left to ``self.checks`` (``_Checks.read``).  Other layouts (CPU tensors, full
+        log-probabilities, int32 evaluate actions) take torch.stack and a read here."""
         assert len(self.logprobs) > 0, \
             "No logprobs were collected because all environments were done. Check your initial state"
+        st = self._status
+        r = None
+        if (st is not None and st.device.type != "cpu" and st.shape[0] >= 2
+                and not self.store_all_logp):
+            ts = nat.torchstep()
+            r = ts.episode_stack(self.actions, self.logprobs, st, True) if ts is not None else None
+            if type(r) is int:
+                nat.check_rc("co_episode_stack", r)
+            if r is None:
+                r = _stack_device(self.actions, self.logprobs, st)
+        if r is not None:
+            actions, logprobs, ll = r
+            logprobs._co_ll = (ll, logprobs._version)
+            if collect and not (self.num_starts > 0 and self.select_best):
+                self.checks = _Checks(st)
+                self._status = None
+                return logprobs, actions, td, env
+            w0 = _Checks(st).read()
+            self._status = None
+            self._finish_checks(logprobs, w0)
+            if self.num_starts > 0 and self.select_best:
+                logprobs, actions, td, env = self._select_best(logprobs, actions, td, env)
+            return logprobs, actions, td, env
         logprobs = torch.stack(self.logprobs, 1)
         actions = torch.stack(self.actions, 1)
         # one host read for the deferred feasibility assert and get_log_likelihood's
@@ -233,7 +339,7 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         ok = ((logprobs > -1000).all() if flat else torch.ones((), dtype=torch.bool,
                                                                 device=logprobs.device))
         ok = ok.to(torch.int32)
-        st = self._status if self._status is not None else torch.zeros_like(ok)
+        st = self._status[0] if self._status is not None else torch.zeros_like(ok)
         words = [st.reshape(()), ok]
         d = nat.pending_deferred(ok.device) if ok.device.type != "cpu" else None
         if d is not None:  # an out-of-range gather_by_index since the last read
@@ -251,12 +357,43 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
             logprobs, actions, td, env = self._select_best(logprobs, actions, td, env)
         return logprobs, actions, td, env
 
+    @staticmethod
+    def _finish_checks(logprobs, w0: int):
+        """After the read: the epilogue's ``> -1000`` test, kept for get_log_likelihood
+        (valid while the tensor is unchanged)."""
+        logprobs._co_logp_ok = (not (w0 & nat.ST_LOGP_NEG_INF), logprobs._version)
+
+    def read_checks(self, logprobs):
+        """The decode loop's single host read (``_post(collect=True)`` left it pending):
+        raises the decode step's and the reward's errors in the reference's order."""
+        checks = getattr(self, "checks", None)
+        if checks is None:
+            return
+        self.checks = None
+        self._finish_checks(logprobs, checks.read())
+
+    def _episode_start(self):
+        """At an episode's first decode step: the step glue's next action / log-probability
+        rows start a slab sized for the episode (``steps_hint``: the env's bound, set by
+        the decode loop), so that ``co_episode_stack`` can take them as one block."""
+        ts = nat.torchstep()
+        if ts is not None:
+            h = getattr(self, "steps_hint", 0)
+            ts.slab_fresh(2 * h + 8 if h else 64)
+
+    def _new_status(self, device):
+        """The strategy's status words (0: the decode steps + epilogue, 1: the env kernels
+        of the decode loop's checks, _Checks)."""
+        return nat.scratch_status(device, 2)
+
     def step(self, logits, mask, td: TensorDict = None, action=None, env=None, **kwargs):
         """``decoding.py:327-369`` as one fused launch."""
         if not self.mask_logits:
             mask = None
         if self._status is None:
-            self._status = nat.scratch_status(logits.device)
+            self._status = self._new_status(logits.device)
+        if self._step_idx == 0:
+            self._episode_start()
         mode = self._mode()
         act_in = action if mode == "evaluate" else None
         seed = getattr(self, "_seed_carry", None)
@@ -307,7 +444,9 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         if mask is not held:
             return None
         if self._status is None:
-            self._status = nat.scratch_status(logits.device)
+            self._status = self._new_status(logits.device)
+        if self._step_idx == 0:
+            self._episode_start()
         seed = int(torch.randint(0, 2**62, ()).item()) if mode == "sampling" else 0
         ain = action if mode == "evaluate" else None
         out = None
@@ -435,7 +574,7 @@ class BeamSearch(DecodingStrategy):
         if not self.mask_logits:
             mask = None
         if self._status is None:
-            self._status = nat.scratch_status(logits.device)
+            self._status = self._new_status(logits.device)
         _, _, full = decode_step(logits, mask, "greedy", self.temperature, self.tanh_clipping,
                                  return_full=True, top_k=self.top_k, top_p=self.top_p)
         e, n = full.shape
@@ -461,7 +600,7 @@ class BeamSearch(DecodingStrategy):
 
     def post_decoder_hook(self, td, env):
         """``decoding.py:558-565``."""
-        if self._status is not None and int(self._status.item()) & nat.ST_INFEASIBLE:
+        if self._status is not None and int(self._status[0].item()) & nat.ST_INFEASIBLE:
             raise AssertionError("infeasible action selected")
         actions, logprobs = self._backtrack()
         if self.select_best:

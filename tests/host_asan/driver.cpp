@@ -112,13 +112,13 @@ static int cvrp(int64_t B, int64_t N) {
 }
 
 static int slap(int64_t B, int64_t L, int64_t P, int64_t O, int64_t K) {
-  std::vector<uint8_t> m0(B * L), m1(B * L), done(B), srw(B);
+  std::vector<uint8_t> m0(B * L), m1(B * L), done(B), srw(B), dn(B), tm(B);
   std::vector<float> tc(B * P), rw(B), ratio(B * L), locs(B * L * 2);
   for (auto& v : locs) v = rf();
   std::vector<int64_t> i0(B), i1(B), act(B), pick(B * O * K);
   std::vector<int32_t> a0(B * P, -1), a1(B * P);
   int32_t st = 0;
-  CHECK(co_slap_reset(B, L, P, m0.data(), tc.data(), i0.data(), rw.data(), ratio.data(), nullptr));
+  CHECK(co_slap_reset(B, L, P, m0.data(), tc.data(), i0.data(), rw.data(), ratio.data(), dn.data(), tm.data(), nullptr));
   for (int64_t t = 0; t < P; ++t) {
     for (int64_t b = 0; b < B; ++b) act[b] = ri(-L - 2, L + 2);  // wraps and out of range
     if (t == 1 && B > 0) tc[0 * P + t] = (float)(P + 3);        // product out of range

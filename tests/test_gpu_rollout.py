@@ -387,3 +387,67 @@ def test_tsp_reward_row_kernel_layouts(dev, n, layout):
     ok[1] = False
     assert ((r[ok] - ref[ok]).abs() <= 1e-5 * ref[ok].abs().clamp(min=1)).all()
     assert int(status.item()) & nat.ST_INVALID_TOUR
+
+
+@pytest.mark.parametrize("n", [20, 100, 112, 130])
+@pytest.mark.parametrize("same_lane", [True, False])
+def test_nearest_sqrt_tie_lane_layouts(dev, n, same_lane):
+    """The fused nearest episodes pick on squared distances and repair ties of the rounded
+    sqrt in a rare exact pass: a sqrt tie whose lower-index node sits before the winner in
+    the SAME lane (node indices 16 apart: the G = 16 lane layout for N <= 128) and in
+    another lane, plus an exact squared-distance tie at two indices, all through the
+    oracle's argmin over rounded distances."""
+    c = torch.tensor([0.5, 0.5])
+    near, far = _sqrt_tie_pair(c)
+    b = 4
+    g = torch.Generator().manual_seed(n)
+    locs = torch.rand(b, n, 2, generator=g) * 0.01 + 5.0  # every other node far away
+    locs[:, 0] = c
+    idx_far = 3
+    idx_near = idx_far + 16 if same_lane else idx_far + 5
+    locs[:, idx_far], locs[:, idx_near] = far, near
+    # an exact tie further on: two nodes at one point, both nearest from the tie pair
+    t1, t2 = (idx_near + 7) % n, (idx_near + 23) % n
+    if t1 not in (0, idx_far, idx_near) and t2 not in (0, idx_far, idx_near, t1):
+        locs[:, t1] = locs[:, t2] = near + torch.tensor([1e-3, 0.0])
+    env = TSPOracle(num_loc=n, seed=1)
+    from oracle.td import TD
+
+    td = env.reset(TD({"locs": locs.clone()}, [b]))
+    r, tdf, a = ref_rollout(env, td, tsp_nearest_action)
+    assert (a[:, 1] == idx_far).all()
+    ep = TSPFusedEpisode(locs.to(dev), None, policy="nearest")
+    ep.run_eager()
+    torch.cuda.synchronize()
+    _check(ep.final_state(), a, r, tdf)
+
+
+@pytest.mark.parametrize("n", [20, 100, 111])
+@pytest.mark.parametrize("same_lane", [True, False])
+def test_cvrp_nearest_sqrt_tie(dev, n, same_lane):
+    """CVRP's fused nearest-feasible episode on the same sqrt-tie construction (customers
+    near / far from the depot whose squared distances differ but round to one f32 sqrt):
+    the lower node index wins, as the oracle's argmin over rounded distances."""
+    from oracle.envs import CVRPOracle, cvrp_nearest_action
+    from oracle.td import TD
+    from rl4co_slap_amd.rollout.engine import CVRPFusedEpisode
+
+    c = torch.tensor([0.5, 0.5])
+    near, far = _sqrt_tie_pair(c)
+    b = 4
+    env = CVRPOracle(num_loc=n, seed=9)
+    gen = env.generate([b])
+    gen["depot"][:] = c
+    gen["locs"] = gen["locs"] * 0.01 + 5.0
+    # node index = customer + 1; 16 apart: one lane of the G = 16 layout
+    cf = 2
+    cn = cf + 16 if same_lane else cf + 5
+    gen["locs"][:, cf - 1], gen["locs"][:, cn - 1] = far, near
+    td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
+    r, tdf, a = ref_rollout(env, td, cvrp_nearest_action)
+    assert (a[:, 0] == cf).all()
+    ep = CVRPFusedEpisode({k: v.to(dev) for k, v in gen.items()},
+                          vehicle_capacity=float(env.vehicle_capacity))
+    ep.run_eager()
+    torch.cuda.synchronize()
+    _check_cvrp(ep.final_state(), a, r, tdf)

@@ -87,6 +87,14 @@ def main():
         cyc = itertools.cycle([e._bound for e in eps])
         wall, ev = bench.timed(lambda: next(cyc)(sh), a.k, 2, 1, dev)
         out = {"launch_us": ev / a.k * 1e6, "wall_us": wall / a.k * 1e6, "batches": n_rot}
+    elif a.mode == "tsp_nearest":  # the fused nearest-policy episode, TSP-100 B = 65,536
+        from rl4co_slap_amd.rollout.engine import TSPFusedEpisode
+
+        locs, _ = bench.tsp_inputs(65536, 100, 0)
+        ep = TSPFusedEpisode(locs.to(dev), None, policy="nearest", check=True)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        wall, ev = bench.timed(lambda: ep._launch(sh), a.k, 2, 1, dev)
+        out = {"ms_per_episode": wall / a.k * 1e3, "launch_ms": ev / a.k * 1e3}
     elif a.mode == "decode_kernels":  # the fused TSP decode step alone, POMO shape, clip 10
         out = {}
         for name, flag in (("certified", _native.DECODE_CERTIFIED), ("fast", _native.DECODE_FAST),
