@@ -654,8 +654,11 @@ def summarize(out):
         sm[name] = {"env_steps_s": r(m["value"], 0), "ms_per_episode": r(m["ms_per_episode"]),
                     "launches_per_step": m.get("launches_per_step"),
                     "gpu_us_per_step": r(m["gpu_ms_per_episode"] * 1e3 / steps, 2),
-                    "host_us_per_step_b64": r(m.get("host_us_per_loop_step_b64",
-                                                    m.get("host_us_per_step_b64")), 2),
+                    # host time per step at B = 64: the whole episode's (reset, reward,
+                    # epilogue included) and the marginal loop step (episodes of P and 2P)
+                    "host_us_per_step_b64_all_in": r(m.get("host_us_per_step_b64"), 2),
+                    "host_us_per_loop_step_b64": r(m.get("host_us_per_loop_step_b64"), 2),
+                    "decode_fused_kernel_us": r(m.get("decode_fused_kernel_us"), 2),
                     "hbm_frac": r(m.get("hbm_frac"))}
     for name in ("pomo_tsp100", "cvrp_fused_nearest", "cvrp_stepwise_graph"):
         m = modes.get(name)
@@ -1093,8 +1096,9 @@ def bench_dropin_slap(b, k, world, rank, dev):
 
 def slap_decode_step_kernel_us(b, dev, reps=50, l=100, p=20):
     """GPU time of one co_slap_decode_step launch (certified greedy, clip 10, the drop-in
-    default) at B x L: a mid-episode state (10 products placed), out-of-place assignment,
-    HIP events over reps launches on the launching stream."""
+    default) at B x L: a mid-episode state (10 products placed) with the operands the step
+    glue passes (the assignment written in place, to_choose's uniform product: no per-row
+    column read), HIP events over reps launches on the launching stream."""
     from rl4co_slap_amd import _native
 
     g = torch.Generator().manual_seed(5)
@@ -1102,20 +1106,19 @@ def slap_decode_step_kernel_us(b, dev, reps=50, l=100, p=20):
     mask = (torch.rand(b, l, generator=g) < 0.9).to(dev)
     mask[:, 0] = False
     mask[:, 1] = True
-    tc = torch.arange(p, dtype=torch.float32).repeat(b, 1).to(dev)
     asg = torch.randint(0, l, (b, p), dtype=torch.int32).to(dev)
     i = torch.full((b, 1), p // 2, dtype=torch.int64, device=dev)
     act = torch.empty(b, dtype=torch.int64, device=dev)
     lp = torch.empty(b, dtype=torch.float32, device=dev)
-    asg_o, m_o = torch.empty_like(asg), torch.empty_like(mask)
+    m_o = torch.empty_like(mask)
     i_o = torch.empty_like(i)
     done, rw = (torch.empty((b, 1), dtype=torch.bool, device=dev) for _ in range(2))
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     sh = torch.cuda.current_stream(dev).cuda_stream
     launch = _native.bind("co_slap_decode_step", b, l, p, logits.data_ptr(), l, mask.data_ptr(),
                           10.0, 1.0, _native.DECODE_CERTIFIED, None, act.data_ptr(),
-                          lp.data_ptr(), 0, 0, tc[:, p // 2:].data_ptr(), p, asg.data_ptr(),
-                          asg_o.data_ptr(), m_o.data_ptr(), i.data_ptr(), i_o.data_ptr(),
+                          lp.data_ptr(), 0, 0, None, p // 2, asg.data_ptr(),
+                          asg.data_ptr(), m_o.data_ptr(), i.data_ptr(), i_o.data_ptr(),
                           done.data_ptr(), rw.data_ptr(), None, st.data_ptr())
     _, ev = timed(lambda: launch(sh), reps, 5, 1, dev)
     return ev / reps * 1e6

@@ -18,6 +18,10 @@ namespace {
 
 constexpr int kNoNode = 0x7fffffff;
 
+#ifndef CO_NEAREST_G8
+#define CO_NEAREST_G8 0  // 1: 8 lanes x 13 slots per instance for N (+1) <= 104 (payload by shuffle)
+#endif
+
 // a constant materialised in a scalar register at its use (an empty asm with an "s"
 // operand): hoisted out of the step loop, the loop's constants otherwise hold VGPRs for
 // the whole kernel, and the CVRP episode needs <= 64 of them for 8 waves per SIMD
@@ -107,6 +111,61 @@ __device__ __forceinline__ int grp_nearest(float cx, float cy, const float (&px)
   return w;
 }
 
+// grp_nearest that also hands every lane of the group the winner's coordinates (and, DEM,
+// its demand): each lane keeps the payload of its own best candidate during the scan (one
+// select per value and candidate) and the owner's is read by one lane shuffle -- no LDS
+// row per instance (the G = 8 engines: 13 slots per lane, whose LDS rows would cap the
+// occupancy).  The rare exact path selects the owner's payload by slot.
+template <int G, int EPL, bool DEM>
+__device__ __forceinline__ int grp_nearest_x(float cx, float cy, const float (&px)[EPL],
+                                             const float (&py)[EPL], const float (&dm)[EPL],
+                                             uint32_t cand, int sl, int gbase, float& m,
+                                             float& wx, float& wy, float& wd) {
+  const float inf = __uint_as_float(su(0x7f800000u));
+  float smin = inf, sbef = inf, bx = 0.f, by = 0.f, bd = 0.f;
+  int kmin = -1;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const float dx = px[k] - cx, dy = py[k] - cy;
+    const float sq = dx * dx + dy * dy;
+    const bool take = ((cand >> k) & 1u) && sq < smin;
+    sbef = take ? smin : sbef;
+    smin = take ? sq : smin;
+    kmin = take ? k : kmin;
+    bx = take ? px[k] : bx;
+    by = take ? py[k] : by;
+    if (DEM) bd = take ? dm[k] : bd;
+  }
+  const uint32_t mb = grp_reduce<G>(__float_as_uint(smin), [](uint32_t a, uint32_t b) {
+    return a < b ? a : b;
+  });
+  const int none = (int)su((uint32_t)kNoNode);
+  const int my = kmin >= 0 ? sl + G * kmin : none;
+  int w = grp_min_int<G>(__float_as_uint(smin) == mb ? my : none);
+  m = __uint_as_float(mb);
+  const float win = m * (1.0f + 0x1p-20f);
+  const bool near = mb < su(0x7f800000u) && ((smin <= win && my < w) || sbef <= win);
+  if (__builtin_expect(__any(near), 0)) {  // a tie of the rounded distances: exact path
+    float best;
+    int bi;
+    lane_nearest<G, EPL>(cx, cy, px, py, cand, sl, best, bi);
+    grp_argmin_split<G>(best, bi);
+    w = bi;
+    const int slot = (w == kNoNode ? 0 : w) / G;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) {
+      bx = k == slot ? px[k] : bx;
+      by = k == slot ? py[k] : by;
+      if (DEM) bd = k == slot ? dm[k] : bd;
+    }
+  }
+  const int src = gbase + (w == none ? 0 : w % G);
+  wx = __shfl(bx, src, 64);
+  wy = __shfl(by, src, 64);
+  if (DEM) wd = __shfl(bd, src, 64);
+  return w;
+}
+
 // The group's value from lane `owner` (`v` of the other lanes is ignored): an OR over the
 // group of the owner's bits, DPP only.
 template <int G>
@@ -120,23 +179,23 @@ __device__ __forceinline__ float grp_from(float v, bool mine) {
 // grid-stride loop: nothing is hoisted across instances, so the kernel stays within 64
 // VGPRs -- 8 waves per SIMD); the group's coordinate row in LDS (8 B per node) gives the
 // chosen node's coordinates as one broadcast read.
-template <int G, int EPL>
+template <int G, int EPL, bool TR>
 __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
     int64_t B, int N, const float2* __restrict__ locs, int64_t* __restrict__ acts_out,
     uint8_t* __restrict__ mask_out, int64_t* __restrict__ first_out,
     int64_t* __restrict__ cur_out, int64_t* __restrict__ i_out, uint8_t* __restrict__ done_out,
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out) {
   constexpr int IPW = 64 / G;
-  __shared__ float2 s_xy[256 * EPL];
+  __shared__ float2 s_xy[TR ? 1 : 256 * EPL];  // TR: the payload comes by lane shuffle
   const int lane = lane_id(), sl = lane % G;
-  float2* xyg = s_xy + (threadIdx.x / G) * (G * EPL);
+  float2* xyg = s_xy + (TR ? 0 : (threadIdx.x / G) * (G * EPL));
   const int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * IPW;
   if (base >= B) return;  // wave-uniform
   const int64_t b = base + lane / G;
   const bool valid = b < B;
   const int64_t bb = valid ? b : B - 1;  // a dead group mirrors the last instance
   const float2* lrow = locs + bb * N;
-  float px[EPL], py[EPL];
+  float px[EPL], py[EPL], nod[EPL];
   uint32_t vis = 0;  // bit k: node sl + G*k visited (or past N)
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
@@ -144,7 +203,7 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
     const float2 q = c < N ? lrow[c] : make_float2(0.f, 0.f);
     px[k] = q.x;
     py[k] = q.y;
-    xyg[c] = q;
+    if (!TR) xyg[c] = q;
     if (c >= N) vis |= 1u << k;
   }
   // the row is written and read by lanes of this wave only: a wave-level fence
@@ -160,11 +219,17 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
   int cur = 0;
   for (int t = 1; t < N; ++t) {
     float m;
-    const int a = grp_nearest<G, EPL>(cx, cy, px, py, ~vis, sl, m);  // t < N: one is left
+    int a;  // t < N: an unvisited node is left
+    if (TR) {
+      float wd;
+      a = grp_nearest_x<G, EPL, false>(cx, cy, px, py, nod, ~vis, sl, lane - sl, m, cx, cy, wd);
+    } else {
+      a = grp_nearest<G, EPL>(cx, cy, px, py, ~vis, sl, m);
+      const float2 q = xyg[a];
+      cx = q.x;
+      cy = q.y;
+    }
     if (sl == a % G) vis |= 1u << (a / G);
-    const float2 q = xyg[a];
-    cx = q.x;
-    cy = q.y;
     len += (double)__builtin_sqrtf(m);
     cur = a;
     if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
@@ -192,7 +257,7 @@ __global__ __launch_bounds__(256) void tsp_nearest_episode_kernel(
 // Coordinates and demand in VGPRs; the chosen node's coordinates from the group's LDS
 // row (8 B per node: with 4 KB of LDS per wave, 8 waves fit per SIMD), its demand from
 // the owner lane's register by a group OR.
-template <int G, int EPL>
+template <int G, int EPL, bool TR>
 __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
     int64_t B, int N, const float2* __restrict__ depot, const float2* __restrict__ locs_in,
     const float* __restrict__ demand, float vcap, int max_steps, int64_t* __restrict__ acts_out,
@@ -202,9 +267,9 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out,
     int32_t* __restrict__ len_out, int32_t* __restrict__ tmax, int32_t* status) {
   constexpr int IPW = 64 / G;
-  __shared__ float2 s_xy[256 * EPL];
+  __shared__ float2 s_xy[TR ? 1 : 256 * EPL];  // TR: the payload comes by lane shuffle
   const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
-  float2* xyg = s_xy + (threadIdx.x / G) * (G * EPL);
+  float2* xyg = s_xy + (TR ? 0 : (threadIdx.x / G) * (G * EPL));
   const int M = N + 1;
   const int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * IPW;
   if (base >= B) return;  // wave-uniform
@@ -230,7 +295,7 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
     px[k] = q.x;
     py[k] = q.y;
     dm[k] = d;
-    xyg[c] = q;
+    if (!TR) xyg[c] = q;
     if (c > N) vis |= 1u << k;
     if (valid && locs_out && c <= N) locs_out[(int64_t)bb * M + c] = q;
   }
@@ -253,17 +318,27 @@ __global__ __launch_bounds__(256) void cvrp_nearest_episode_kernel(
       const bool feas = c >= 1 && !((vis >> k) & 1u) && !(dm[k] + used > vcap);
       cand |= (uint32_t)feas << k;
     }
-    float m;
-    const int bi = grp_nearest<G, EPL>(cx, cy, px, py, cand, sl, m);
-    const int a = bi == kNoNode ? 0 : bi;
-    const int owner = a % G, slot = a / G;
-    float dsel = 0.f;  // the owner lane's demand of node a
+    float m, ad;
+    int a;
+    float2 q;
+    if (TR) {
+      float wx, wy;
+      const int bi = grp_nearest_x<G, EPL, true>(cx, cy, px, py, dm, cand, sl, gbase, m, wx, wy,
+                                                 ad);
+      a = bi == kNoNode ? 0 : bi;
+      q = a == 0 ? dep : make_float2(wx, wy);
+    } else {
+      const int bi = grp_nearest<G, EPL>(cx, cy, px, py, cand, sl, m);
+      a = bi == kNoNode ? 0 : bi;
+      const int slot = a / G;
+      float dsel = 0.f;  // the owner lane's demand of node a
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) dsel = k == slot ? dm[k] : dsel;
-    const float ad = grp_from<G>(dsel, sl == owner);
+      for (int k = 0; k < EPL; ++k) dsel = k == slot ? dm[k] : dsel;
+      ad = grp_from<G>(dsel, sl == a % G);
+      q = xyg[a];
+    }
     if (done) continue;
-    if (sl == owner) vis |= 1u << slot;
-    const float2 q = xyg[a];
+    if (sl == a % G) vis |= 1u << (a / G);
     const float dx = q.x - cx, dy = q.y - cy;  // = m for a customer (same operations)
     dist += (double)__builtin_sqrtf(dx * dx + dy * dy);
     used = a != 0 ? (used + ad) * 1.0f : 0.0f;  // cvrp/env.py:83-85
@@ -344,11 +419,13 @@ int co_internal_tsp_nearest_rollout(int64_t B, int64_t N, const float* locs, int
   hipStream_t s = (hipStream_t)stream;
   if (group_grid(B, 64) == 0) return CO_E_INVAL;
 #define CO_TSPN(G, EPL)                                                                        \
-  hipLaunchKernelGGL((tsp_nearest_episode_kernel<G, EPL>), dim3(group_grid(B, G)), dim3(256),  \
+  hipLaunchKernelGGL((tsp_nearest_episode_kernel<G, EPL, (G <= 8 && EPL > 8)>),                \
+                     dim3(group_grid(B, G)), dim3(256),                                         \
                      0, s, B, (int)N, l2, acts_out, mask_out, first_out, cur_out, i_out,       \
                      done_out, step_reward_out, reward_out)
   if (N <= 32) CO_TSPN(4, 8);
   else if (N <= 64) CO_TSPN(8, 8);
+  else if (CO_NEAREST_G8 && N <= 104) CO_TSPN(8, 13);
   else if (N <= 112) CO_TSPN(16, 7);
   else if (N <= 128) CO_TSPN(16, 8);
   else if (N <= 256) CO_TSPN(32, 8);
@@ -383,13 +460,15 @@ extern "C" int co_cvrp_rollout(int64_t B, int64_t N, const float* depot, const f
   const float2* l2 = reinterpret_cast<const float2*>(locs);
   float2* lo = reinterpret_cast<float2*>(locs_out);
 #define CO_CVRPN(G, EPL)                                                                       \
-  hipLaunchKernelGGL((cvrp_nearest_episode_kernel<G, EPL>), dim3(group_grid(B, G)), dim3(256), \
+  hipLaunchKernelGGL((cvrp_nearest_episode_kernel<G, EPL, (G <= 8 && EPL > 8)>),               \
+                     dim3(group_grid(B, G)), dim3(256),                                         \
                      0, s, B, (int)N, d2, l2, demand, vcap, (int)max_steps, acts_out, lo,      \
                      cur_out, used_out, vcap_out, visited_out, mask_out, done_out,             \
                      step_reward_out, reward_out, len_out, steps_out, status)
   const int64_t M = N + 1;
   if (M <= 32) CO_CVRPN(4, 8);
   else if (M <= 64) CO_CVRPN(8, 8);
+  else if (CO_NEAREST_G8 && M <= 104) CO_CVRPN(8, 13);
   else if (M <= 112) CO_CVRPN(16, 7);
   else if (M <= 128) CO_CVRPN(16, 8);
   else if (M <= 256) CO_CVRPN(32, 8);

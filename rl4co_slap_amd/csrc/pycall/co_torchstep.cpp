@@ -89,6 +89,20 @@ at::Tensor view_of(const c10::Storage& st, at::ScalarType dt, int64_t off_bytes,
   return at::Tensor(std::move(impl));
 }
 
+// t[:, 1:] of a 2-D tensor without a dispatcher call (at::slice costs ~1 us of host time
+// per step): a TensorImpl over the same storage, one element further, that shares t's
+// version counter -- as a view does, so an in-place write through either is seen by the
+// other's version (the env's host-side records on to_choose stay sound).
+at::Tensor drop_first_col(const at::Tensor& t) {
+  auto impl = c10::make_intrusive<c10::TensorImpl>(
+      c10::Storage(t.storage()), c10::DispatchKeySet(c10::DispatchKey::CUDA), t.dtype());
+  const int64_t sizes[2] = {t.size(0), t.size(1) - 1}, strides[2] = {t.stride(0), t.stride(1)};
+  impl->set_sizes_and_strides(c10::IntArrayRef(sizes, 2), c10::IntArrayRef(strides, 2));
+  impl->set_storage_offset(t.storage_offset() + t.stride(1));
+  impl->set_version_counter(t.unsafeGetTensorImpl()->version_counter());
+  return at::Tensor(std::move(impl));
+}
+
 c10::Storage new_storage(const c10::Device& dev, int64_t nbytes) {
   return at::empty({nbytes}, at::TensorOptions().dtype(at::kByte).device(dev)).storage();
 }
@@ -514,7 +528,7 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     Py_END_ALLOW_THREADS
     if (rc != CO_OK) return PyLong_FromLong(rc);
     if (in_place) asg.unsafeGetTensorImpl()->bump_version();  // an in-place write
-    PyObject* tc_next = THPVariable_Wrap(tc.slice(1, 1));  // to_choose[:, 1:] (a view)
+    PyObject* tc_next = THPVariable_Wrap(drop_first_col(tc));  // to_choose[:, 1:]
     if (!tc_next) return nullptr;
     if (uniform && remember(tc_next, g_attr_tc, ktc + 1)) {
       Py_DECREF(tc_next);

@@ -631,6 +631,10 @@ __host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O
 #define CO_SLAP_LATE 0  // 1: the coordinates, 2: also the picklist loaded after the step loop
 #endif
 
+#ifndef CO_SLAP_POP
+#define CO_SLAP_POP 1  // closest-free step loop: branch-free pop (0: the owner's branch)
+#endif
+
 #ifndef CO_SLAP_WPE
 #define CO_SLAP_WPE 0  // > 0: amdgpu_waves_per_eu floor (SGPRs cap the kernel at 7 waves)
 #endif
@@ -741,6 +745,26 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
 #pragma unroll
     for (int k = 2; k < EPL; ++k) s_keys[k * 64 + lane] = key[k];
     int h = 2;
+#if CO_SLAP_POP
+    // branch-free pop: every lane reads the key after its `next` each step (issued before
+    // the two group reductions, so its latency hides behind them) and the owner's head /
+    // next / free bit move by selects -- no divergent branch and exec-mask juggling per step
+    for (int t = 0; t < P; ++t) {
+      const uint64_t nn = h < EPL ? s_keys[h * 64 + lane] : ~0ull;
+      const uint32_t hh = (uint32_t)(hk >> 32);
+      const uint32_t gm = grp_reduce<G>(hh, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+      const uint32_t cand = hh == gm ? (uint32_t)hk : 0xffffffffu;
+      const uint32_t gi =
+          grp_reduce<G>(cand, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+      const bool any = gm < kOrdInf;
+      const bool pop = any && (uint32_t)hk == gi;  // the owner's head is the chosen location
+      avail &= pop ? ~(1u << (gi / G)) : ~0u;
+      hk = pop ? nk : hk;
+      nk = pop ? nn : nk;
+      h += pop ? 1 : 0;
+      if (sl == 0) asg[t] = any ? (int32_t)gi : 0;  // product t
+    }
+#else
     for (int t = 0; t < P; ++t) {
       const uint32_t hh = (uint32_t)(hk >> 32);
       const uint32_t gm = grp_reduce<G>(hh, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
@@ -756,6 +780,7 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
       }
       if (sl == 0) asg[t] = any ? (int32_t)gi : 0;  // product t
     }
+#endif
   } else {
     // teacher actions: lane sl loads steps t = sl, sl + G, ... (all loads in flight at
     // once, a few VGPRs), writes the int32 assignment entry and the wrapped location (-1

@@ -131,6 +131,7 @@ class ConstructivePolicy(nn.Module):
         step = 0
         decode = _direct_call(self.decoder)
         poll = getattr(env, "poll_done", None) or (lambda t: (bool(t["done"].all()), 1))
+        fast = None  # greedy through the env's native glue: the per-step decisions bound once
         while True:
             if step >= lb:  # the reference's `while not td["done"].all()` test
                 done, k = poll(td)
@@ -138,14 +139,17 @@ class ConstructivePolicy(nn.Module):
                     break
                 lb = step + k  # cannot be all done before then: no host sync until
             logits, mask = decode(td, hidden, num_starts)
-            act = actions[..., step] if actions is not None else None
-            # decode + env step as one launch where the env provides it (TSP, CVRP, SLAP)
-            nxt = strategy.step_env_fused(logits, mask, td, env, action=act)
-            if nxt is None:
-                td = strategy.step(logits, mask, td, action=act)
-                td = env.step(td)["next"]
-            else:
-                td = nxt
+            if fast is None or not fast(td, logits, mask):
+                act = actions[..., step] if actions is not None else None
+                # decode + env step as one launch where the env provides it (TSP, CVRP, SLAP)
+                nxt = strategy.step_env_fused(logits, mask, td, env, action=act)
+                if nxt is None:
+                    td = strategy.step(logits, mask, td, action=act)
+                    td = env.step(td)["next"]
+                else:
+                    td = nxt
+                    if step == 0 and actions is None:
+                        fast = strategy.fast_stepper(env)
             step += 1
             if step > max_steps:
                 log.error(f"Exceeded maximum number of steps ({max_steps}) duing decoding")

@@ -175,22 +175,29 @@ def rollout(env, td, policy, max_steps: int = None):
 def _stack_device(actions, logprobs, status):
     """``torch.stack(actions, 1)`` / ``torch.stack(logprobs, 1)`` + the log-likelihood
     sum and the ``> -1000`` test through ``co_episode_stack`` on step-major stacks (the
-    same kernel, so the same bits, as the step glue's slab path); None when the per-step
-    tensors are not [B] int64 / f32 device tensors of one device."""
-    a0, l0 = actions[0], logprobs[0]
-    if (a0.dim() != 1 or l0.dim() != 1 or a0.dtype != torch.int64 or l0.dtype != torch.float32
-            or a0.device != status.device or l0.device != status.device):
+    same kernel, so the same bits, as the step glue's slab path); int64 actions ride along,
+    others (int32 evaluate actions) are stacked by torch.  None when the per-step
+    log-probabilities are not [B] f32 tensors on the status word's device."""
+    l0 = logprobs[0]
+    if l0.dim() != 1 or l0.dtype != torch.float32 or l0.device != status.device:
         return None
-    A = torch.stack(actions, 0)  # [T, B]: rows are the steps' tensors (checks shapes too)
-    L = torch.stack(logprobs, 0)
-    if A.shape != L.shape or A.dtype != torch.int64 or L.dtype != torch.float32:
-        return None
-    t, b = A.shape
-    acts = torch.empty((b, t), dtype=torch.int64, device=A.device)
-    lps = torch.empty((b, t), dtype=torch.float32, device=A.device)
-    ll = torch.empty(b, dtype=torch.float32, device=A.device)
-    nat.call("co_episode_stack", b, t, nat.ptr(A), b, nat.ptr(L), b, nat.ptr(acts),
-             nat.ptr(lps), nat.ptr(ll), nat.ptr(status), nat.stream_of(A))
+    L = torch.stack(logprobs, 0)  # [T, B]: rows are the steps' tensors (checks shapes too)
+    t, b = L.shape
+    dev = L.device
+    a0 = actions[0]
+    A = None
+    if a0.dim() == 1 and a0.dtype == torch.int64 and a0.device == dev:
+        A = torch.stack(actions, 0)
+        if A.shape != L.shape:
+            return None
+        acts = torch.empty((b, t), dtype=torch.int64, device=dev)
+    else:
+        acts = torch.stack(actions, 1)
+    lps = torch.empty((b, t), dtype=torch.float32, device=dev)
+    ll = torch.empty(b, dtype=torch.float32, device=dev)
+    nat.call("co_episode_stack", b, t, nat.ptr(A), b, nat.ptr(L), b,
+             nat.ptr(acts) if A is not None else None, nat.ptr(lps), nat.ptr(ll),
+             nat.ptr(status), nat.stream_of(L))
     return acts, lps, ll
 
 
@@ -467,6 +474,38 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
         self.actions.append(sel)
         self.logprobs.append(logp)
         return td
+
+    def fast_stepper(self, env):
+        """After a greedy loop's first fused step through the env's native glue: a closure
+        ``f(td, logits, mask) -> bool`` for the following steps with everything
+        ``step_env_fused`` decides per call bound once (the glue, mode word, temperature,
+        clipping, status word, the action / log-probability lists).  It returns False,
+        having done nothing, whenever the fused path does not apply to a call (the caller
+        then takes ``step_env_fused``); None when there is nothing to bind."""
+        cached = self._fused
+        if (cached is None or cached[0] is not env or cached[1] is None or cached[2] is None
+                or cached[3] != "greedy" or getattr(env, "_torchrl_mode", False)
+                or self._status is None or self._step_idx == 0):
+            return None
+        native, mword = cached[2], cached[4]
+        temp, clip, key, st = self.temperature, self.tanh_clipping, self.key, self._status
+        push_a, push_l = self.actions.append, self.logprobs.append
+        dget, td_type = dict.get, TensorDict
+
+        def stepper(td, logits, mask):
+            if type(td) is not td_type or mask is not dget(td, "action_mask"):
+                return False
+            out = native(td, logits, mword, temp, clip, None, 0, self._step_idx, st, key)
+            if out is None:
+                return False
+            if type(out) is int:
+                nat.check_rc("decode_and_step", out)
+            self._step_idx += 1
+            push_a(out[0])
+            push_l(out[1])
+            return True
+
+        return stepper
 
     @abc.abstractmethod
     def _mode(self) -> str:

@@ -1,0 +1,170 @@
+"""The decode loop's epilogue (``co_episode_stack``: DecodingStrategy.post_decoder_hook's two
+torch.stack calls, get_log_likelihood's sum and its ``> -1000`` assert, decoding.py:39-65,
+315-325) and the episode-level host plumbing around it: the step glue's slabs, the single
+status read shared with the reward, the reused zero status words, the SLAP reset in one
+launch, and the SLAP step's in-place assignment / uniform product."""
+import numpy as np
+import pytest
+import torch
+
+from rl4co_slap_amd import TensorDict
+from rl4co_slap_amd import _native as nat
+from rl4co_slap_amd.envs import CVRPEnv, SLAPEnv, TSPEnv
+from rl4co_slap_amd.envs.slap import SLAPGenerator
+from rl4co_slap_amd.rollout import ConstructivePolicy
+from rl4co_slap_amd.rollout.constructive import LogitsDecoder
+from rl4co_slap_amd.utils.decoding import get_log_likelihood
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("b,t", [(1, 1), (5, 3), (64, 20), (100, 33), (1000, 199), (65, 64)])
+def test_episode_stack_matches_torch(dev, b, t):
+    g = torch.Generator().manual_seed(b * 7 + t)
+    rs = b + 13  # row stride past B (the glue's slab rows are padded)
+    acts = torch.randint(0, 1000, (t, rs), generator=g).to(dev)
+    lps = (-torch.rand(t, rs, generator=g) * 5).to(dev)
+    out_a = torch.empty(b, t, dtype=torch.int64, device=dev)
+    out_l = torch.empty(b, t, dtype=torch.float32, device=dev)
+    ll = torch.empty(b, dtype=torch.float32, device=dev)
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    nat.call("co_episode_stack", b, t, nat.ptr(acts), rs, nat.ptr(lps), rs, nat.ptr(out_a),
+             nat.ptr(out_l), nat.ptr(ll), nat.ptr(st), nat.stream_of(acts))
+    torch.cuda.synchronize()
+    assert torch.equal(out_a, acts[:, :b].t())
+    assert torch.equal(out_l, lps[:, :b].t())
+    ref = lps[:, :b].double().sum(0).float()  # an f64 sum, rounded once (within 1 ulp)
+    assert ((ll - ref).abs() <= ref.abs() * 2.0 ** -23).all()
+    assert ((ll - out_l.sum(1)).abs() <= 1e-5 * out_l.sum(1).abs().clamp(min=1)).all()
+    assert int(st.item()) == 0
+    # the `> -1000` test: -inf and NaN fail it
+    for bad in (float("-inf"), float("nan"), -1000.0):
+        lps2 = lps.clone()
+        lps2[t - 1, b - 1] = bad
+        st.zero_()
+        nat.call("co_episode_stack", b, t, nat.ptr(acts), rs, nat.ptr(lps2), rs, nat.ptr(out_a),
+                 nat.ptr(out_l), nat.ptr(ll), nat.ptr(st), nat.stream_of(acts))
+        assert int(st.item()) == nat.ST_LOGP_NEG_INF, bad
+
+
+def test_episode_stack_validation(dev):
+    lib = nat.load()
+    # a row stride below B, actions without an output: rejected before any launch
+    assert lib.co_episode_stack(4, 3, 1, 2, None, 0, None, None, None, None, None) == -1
+    assert lib.co_episode_stack(4, 3, 1, 4, None, 0, None, None, None, None, None) == -1
+    assert lib.co_episode_stack(0, 3, None, 0, None, 0, None, None, None, None, None) == 0
+
+
+def _slap_data(b, dev, seed=1234):
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    return SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
+
+
+@pytest.mark.parametrize("decode_type", ["greedy", "sampling", "evaluate"])
+def test_slap_glue_episode_equals_python_path(dev, decode_type, monkeypatch):
+    """The whole SLAP drop-in episode with the step glue (one-launch reset, slab rows +
+    co_episode_stack, in-place assignment, uniform product, one status read) against the
+    Python path (every tensor fresh, torch.stack + co_episode_stack on the stacks): actions,
+    log-likelihood, reward, final assignment / mask / i bit for bit."""
+    b = 96
+    data = _slap_data(b, dev)
+    logits = torch.randn(b, 100, generator=torch.Generator().manual_seed(3)).to(dev)
+    acts = None
+    outs = []
+    for glue in (True, False):
+        if not glue:
+            monkeypatch.setattr(nat, "_tstep", False)
+        env = SLAPEnv(device=dev)
+        td = env.reset(TensorDict(dict(data.items()), [b]))
+        assert td["done"].shape == (b, 1) and not td["done"].any() and not td["terminated"].any()
+        pol = ConstructivePolicy(None, LogitsDecoder(lambda t: logits), env_name="slap",
+                                 tanh_clipping=10.0)
+        torch.manual_seed(77)
+        kw = {"decode_type": decode_type}
+        if decode_type == "evaluate":
+            if acts is None:
+                acts = ConstructivePolicy(None, LogitsDecoder(lambda t: logits), env_name="slap")(
+                    env.reset(TensorDict(dict(data.items()), [b])), env, decode_type="greedy",
+                    return_actions=True)["actions"]
+            kw = {"actions": acts}
+        out = pol(td, env, phase="test", return_actions=True, **kw)
+        outs.append((out, {k: td[k].clone() for k in ("assignment", "action_mask", "i", "done")}))
+        monkeypatch.undo()
+    (a, sa), (b_, sb) = outs
+    for k in ("actions", "log_likelihood", "reward"):
+        assert torch.equal(a[k], b_[k]), k
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    # the caller's assignment is never written (the first step copies it)
+    assert (data["assignment"] == -1).all()
+
+
+def test_slap_inplace_assignment_only_when_unshared(dev):
+    """The glue writes the assignment in place only when nothing but the td holds it: the
+    first step copies the caller's tensor, the next ones reuse the td's own; a reference
+    the caller keeps makes the next step copy again, and the kept tensor never changes."""
+    from rl4co_slap_amd.utils.decoding import Greedy
+
+    b = 32
+    data = _slap_data(b, dev, 5)
+    env = SLAPEnv(device=dev)
+    td = env.reset(TensorDict(dict(data.items()), [b]))
+    logits = torch.randn(b, 100, generator=torch.Generator().manual_seed(4)).to(dev)
+    s = Greedy()
+    ptrs = []
+    for _ in range(3):
+        assert s.step_env_fused(logits, td["action_mask"], td, env) is not None
+        ptrs.append(td["assignment"].data_ptr())
+    assert ptrs[0] != data["assignment"].data_ptr()  # the caller's tensor: copied
+    assert ptrs[1] == ptrs[0] and ptrs[2] == ptrs[0]  # the td's own: in place
+    kept = td["assignment"]
+    snap = kept.clone()
+    assert s.step_env_fused(logits, td["action_mask"], td, env) is not None
+    torch.cuda.synchronize()
+    assert td["assignment"].data_ptr() != kept.data_ptr()
+    assert torch.equal(kept, snap)
+    assert (data["assignment"] == -1).all()
+
+
+def test_status_words_reused_only_when_zero(dev):
+    w = nat.scratch_status(dev, 2)
+    nat.release_status(w, [0, 0])
+    assert nat.scratch_status(dev, 2) is w
+    w2 = nat.scratch_status(dev, 2)
+    w2[0] = 4
+    nat.release_status(w2, [4, 0])
+    assert nat.scratch_status(dev, 2) is not w2
+
+
+@pytest.mark.parametrize("env_cls", [TSPEnv, CVRPEnv])
+def test_glue_epilogue_routing_tsp_cvrp(dev, env_cls):
+    """TSP / CVRP drop-in episodes take the slab epilogue too: the log-likelihood comes back
+    from co_episode_stack (cached on the logprobs) and equals the f64 step-order sum."""
+    b, n = 50, 20
+    g = torch.Generator().manual_seed(8)
+    if env_cls is TSPEnv:
+        data = {"locs": torch.rand(b, n, 2, generator=g).to(dev)}
+        na = n
+    else:
+        la = torch.rand(b, n + 1, 2, generator=g)
+        data = {"depot": la[:, 0].contiguous().to(dev), "locs": la[:, 1:].contiguous().to(dev),
+                "demand": (((torch.rand(b, n, generator=g) * 9).int() + 1).float() / 30.0).to(dev)}
+        na = n + 1
+    logits = torch.randn(b, na, generator=g).to(dev)
+    env = env_cls(generator_params=dict(num_loc=n), device=dev)
+    td = env.reset(TensorDict(dict(data), [b]))
+    from rl4co_slap_amd.utils import decoding as D
+
+    s = D.Greedy()
+    s.steps_hint = n
+    steps = 0
+    while not bool(td["done"].all()):
+        assert s.step_env_fused(logits, td["action_mask"], td, env) is not None
+        steps += 1
+    lps, acts, td, env = s.post_decoder_hook(td, env)
+    assert getattr(lps, "_co_ll", None) is not None
+    ll = get_log_likelihood(lps, acts)
+    ref = lps.double().sum(1).float()
+    assert ((ll - ref).abs() <= ref.abs() * 2.0 ** -23).all()
+    assert acts.shape == (b, steps)

@@ -409,7 +409,7 @@ def test_nearest_sqrt_tie_lane_layouts(dev, n, same_lane):
     # an exact tie further on: two nodes at one point, both nearest from the tie pair
     t1, t2 = (idx_near + 7) % n, (idx_near + 23) % n
     if t1 not in (0, idx_far, idx_near) and t2 not in (0, idx_far, idx_near, t1):
-        locs[:, t1] = locs[:, t2] = near + torch.tensor([1e-3, 0.0])
+        locs[:, t1] = locs[:, t2] = c + (near - c) * 1.01  # radially beyond the pair
     env = TSPOracle(num_loc=n, seed=1)
     from oracle.td import TD
 

@@ -52,9 +52,15 @@ res = {}
 sink = torch.zeros(256, dtype=torch.int32, device=dev)
 src = torch.ones(2048 * 256, dtype=torch.int32, device=dev)
 dst = torch.empty_like(src)
-res["empty_2048x256"] = ev_us(lambda: lc.ceiling_empty(2048, 256, 1, sink.data_ptr(), sh))
-res["touch_2048x256_4MB"] = ev_us(lambda: lc.ceiling_touch(2048, 256, 1, src.data_ptr(),
-                                                           dst.data_ptr(), sh))
+# the same 512K threads as 2,048 x 256 (the step kernels' grid) and in other workgroup sizes:
+# how much of a one-round launch is the workgroup dispatch
+for blocks, threads in ((2048, 256), (8192, 64), (4096, 128), (1024, 512), (512, 1024)):
+    res[f"empty_{blocks}x{threads}"] = ev_us(
+        lambda: lc.ceiling_empty(blocks, threads, 1, sink.data_ptr(), sh))
+    res[f"touch_{blocks}x{threads}_4MB"] = ev_us(
+        lambda: lc.ceiling_touch(blocks, threads, 1, src.data_ptr(), dst.data_ptr(), sh))
+res["empty_256x256"] = ev_us(lambda: lc.ceiling_empty(256, 256, 1, sink.data_ptr(), sh))
+res["empty_1x64"] = ev_us(lambda: lc.ceiling_empty(1, 64, 1, sink.data_ptr(), sh))
 
 
 def copy_us(nbytes):

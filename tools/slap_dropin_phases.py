@@ -121,3 +121,60 @@ st = torch.zeros(1, dtype=torch.int32, device=dev)
 unit["nat.call co_zero_i32-like (scratch_status)"] = us(lambda: nat.scratch_status(dev))
 res["unit_us"] = unit
 print(json.dumps(res), flush=True)
+
+# ---- the loop step's pieces at this batch (us per call) -----------------------------
+from rl4co_slap_amd.utils.decoding import Greedy  # noqa: E402
+
+ts = nat.torchstep()
+st2 = nat.scratch_status(dev, 2)
+
+
+def steps_us(make_step, episodes=100, steps=19):
+    """host us per call of make_step(td)() over `steps` calls per fresh reset (the reset
+    itself outside the timed region)"""
+    tot = 0.0
+    for e in range(episodes + 5):
+        t_ = env.reset(TensorDict(dict(data.items()), [b]))
+        f = make_step(t_)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            f()
+        if e >= 5:
+            tot += time.perf_counter() - t0
+    torch.cuda.synchronize()
+    return round(tot / episodes / steps * 1e6, 3)
+
+
+piece = {}
+piece["glue slap_step_td"] = steps_us(lambda t_: (lambda: ts.slap_step_td(
+    env._lb_attr, t_, logits, nat.DECODE_CERTIFIED, 1.0, 10.0, None, 0, 1, st2, "action")))
+
+
+def fused_step(t_):
+    sg = Greedy(tanh_clipping=10.0)
+    sg._status = st2
+    sg._step_idx = 1  # past the episode start
+    return lambda: sg.step_env_fused(logits, t_["action_mask"], t_, env)
+
+
+piece["strategy.step_env_fused"] = steps_us(fused_step)
+td = env.reset(TensorDict(dict(data.items()), [b]))
+dec = pol.decoder
+piece["decoder(td)"] = us(lambda: dec(td, None, 0), 2000)
+m, i_t = td["action_mask"], td["i"]
+a_out = torch.empty(b, dtype=torch.int64, device=dev)
+lp_out = torch.empty(b, dtype=torch.float32, device=dev)
+asg = td["assignment"]
+outs = [torch.empty_like(m), torch.empty_like(i_t), torch.empty((b, 1), dtype=torch.bool, device=dev),
+        torch.empty((b, 1), dtype=torch.bool, device=dev)]
+args = (b, 100, 20, logits.data_ptr(), 100, m.data_ptr(), 10.0, 1.0, nat.DECODE_CERTIFIED, None,
+        a_out.data_ptr(), lp_out.data_ptr(), 0, 1, None, 5, asg.data_ptr(), asg.data_ptr(),
+        outs[0].data_ptr(), i_t.data_ptr(), outs[1].data_ptr(), outs[2].data_ptr(),
+        outs[3].data_ptr(), None, st2.data_ptr())
+launch = nat.bind("co_slap_decode_step", *args)
+sh = nat.stream_of(m)
+piece["bind launch (ctypes, preconverted)"] = us(lambda: launch(sh), 2000)
+piece["nat.call co_slap_decode_step B=0 (no launch)"] = us(
+    lambda: nat.call("co_slap_decode_step", 0, *args[1:], sh), 2000)
+piece["nat.call co_slap_decode_step"] = us(lambda: nat.call("co_slap_decode_step", *args, sh), 2000)
+print(json.dumps({"batch": b, "pieces_us": piece}), flush=True)
