@@ -235,7 +235,7 @@ int co_tsp_decode_step(int64_t batch, int64_t num_loc, const float* logits,
  * action_in, negative values index from the end as python indexing):
  *   assign_out = assign_in with [b, (int)to_choose[b*tc_stride]] = (int)a (out of place:
  *   the row is copied; in place: that element only); mask_out = mask_in minus a
- *   (in-place NOT allowed); done[b] = i_in[b] == P-1; i_out = i_in + 1; step_reward = 0;
+ *   (in place allowed, as i_out = i_in); done[b] = i_in[b] == P-1; i_out = i_in + 1; step_reward = 0;
  *   ll_accum (nullable) += logp_sel.  Same bits as co_decode_step + co_slap_step. */
 int co_slap_decode_step(int64_t batch, int64_t num_slots, int64_t n_products,
                         const float* logits, int64_t logits_stride, const uint8_t* mask_in,

@@ -467,7 +467,8 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
       !i_out || !done || !step_reward || (mode == CO_DECODE_EVALUATE && !action_in) ||
       (!to_choose && (tc_stride < 0 || tc_stride >= P)))
     return CO_E_INVAL;
-  if (mask_out == mask_in) return CO_E_INVAL;  // the mask is read by other lanes' decode
+  // mask_out may be mask_in: a row's mask is read (and re-read by the certified fallback)
+  // by its own lane group before the transition stores it, after the wave's stage barrier
   const int64_t N = L;  // the row-dispatch macros' name for the row length
   const int rpw = 64 / row_lanes(N);
   const size_t shmem = (size_t)4 * slap_stage_dwords(rpw, (int)P) * 4;

@@ -426,6 +426,15 @@ inline PyObject* td_tensor(PyObject* td, const char* k) {  // borrowed; nullptr 
   return (o && is_tensor(o)) ? o : nullptr;
 }
 
+// td[k] = a new Python object of t (the tensor moved into it); -1 on error
+inline int set_wrapped(PyObject* td, const char* k, at::Tensor& t) {
+  PyObject* o = THPVariable_Wrap(std::move(t));
+  if (!o) return -1;
+  const int err = PyDict_SetItemString(td, k, o);
+  Py_DECREF(o);
+  return err;
+}
+
 // True when `o` (a tensor the td dict holds) is referenced by nothing but that dict: one
 // Python reference, one at::Tensor handle, a storage of its own (no views, no pool), no
 // autograd.  Writing it in place then cannot be told apart from writing a fresh copy.
@@ -434,19 +443,54 @@ inline bool exclusively_held(PyObject* o, const at::Tensor& t) {
          !t.requires_grad() && t.is_contiguous() && t.storage_offset() == 0;
 }
 
+// The SLAP step's state block: action_mask [B, L], i [B, 1], done [B, 1], reward [B, 1]
+// carved from one storage of their own (not pooled).  When the td holds the block a
+// previous step made and nothing else refers to any of it -- one Python reference and one
+// at::Tensor handle per tensor, the storage referenced by exactly these four -- the next
+// step rewrites it in place: indistinguishable from fresh outputs (nothing can observe the
+// old values), and a step then makes two tensors (action, log-probability) instead of
+// six.  Otherwise a new block is carved.
+struct SlapBlock {
+  int64_t om, oi, od, orw, nbytes;
+  SlapBlock(int64_t b, int64_t l) {
+    Carver c;
+    om = c.take(b * l);
+    oi = c.take(8 * b);
+    od = c.take(b);
+    orw = c.take(b);
+    nbytes = c.off;
+  }
+  bool held_alone(PyObject* const (&o)[4], const at::Tensor* const (&t)[4], int64_t b,
+                  int64_t l) const {
+    const c10::StorageImpl* sti = t[0]->storage().unsafeGetStorageImpl();
+    if (t[0]->storage().use_count() != 4 || t[0]->storage().nbytes() != (size_t)nbytes) return false;
+    const int64_t offs[4] = {om, oi / 8, od, orw};
+    const at::ScalarType dts[4] = {at::kBool, at::kLong, at::kBool, at::kBool};
+    for (int k = 0; k < 4; ++k) {
+      const at::Tensor& x = *t[k];
+      if (Py_REFCNT(o[k]) != 1 || x.use_count() != 1 || x.requires_grad() ||
+          x.storage().unsafeGetStorageImpl() != sti || x.scalar_type() != dts[k] ||
+          x.storage_offset() != offs[k] || !x.is_contiguous() || x.dim() != 2 || x.size(0) != b ||
+          x.size(1) != (k == 0 ? l : 1))
+        return false;
+    }
+    return true;
+  }
+};
+
 // slap_step_td(fn, lb_attr, td, logits, mode, temp, clip, action_in, seed, offset, status,
 //              key) -> (action, logp) | None | error code
 // SLAPEnv.decode_and_step (envs/slap.py) on a dict-backed TensorDict in one call: reads
-// action_mask / i / to_choose / assignment / freq, launches co_slap_decode_step into fresh
-// outputs, stores assignment / to_choose[:, 1:] / action_mask / i / reward / done and the
-// action, records the done lower bound on the new i.  Two traffic savings, both invisible
-// to the caller:
+// action_mask / i / to_choose / assignment / freq, launches co_slap_decode_step, stores
+// assignment / to_choose[:, 1:] / action_mask / i / reward / done and the action, records
+// the done lower bound on the new i.  Savings invisible to the caller:
 // * to_choose that is still the env's untouched arange (record "_co_tc" = k, version
 //   unchanged) is not read: the kernel takes the uniform product k (co_env.h);
 // * the assignment is the reference's clone with one element changed (slap/env.py:50-54):
 //   when nothing but the td refers to the input assignment, that element is written in
 //   place; otherwise the row is copied into a new storage of its own (so the next step can
-//   write it in place).
+//   write it in place);
+// * the state block (SlapBlock) likewise: in place when held by the td alone.
 PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
   if (n != 12) {
     PyErr_SetString(PyExc_TypeError, "slap_step_td: 12 arguments");
@@ -461,11 +505,13 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     Py_RETURN_NONE;
   PyObject *mask_o = td_tensor(td, "action_mask"), *i_o = td_tensor(td, "i"),
            *tc_o = td_tensor(td, "to_choose"), *as_o = td_tensor(td, "assignment"),
-           *fr_o = td_tensor(td, "freq");
+           *fr_o = td_tensor(td, "freq"), *dn_o = td_tensor(td, "done"),
+           *rw_o = td_tensor(td, "reward");
   if (!mask_o || !i_o || !tc_o || !as_o || !fr_o) Py_RETURN_NONE;
   const auto fn = fn_at<SlapDecodeStep>(a[0]);
   const long long ki = known(i_o, g_attr_i);
   const long long ktc = known(tc_o, g_attr_tc);
+  const long long lb = known(i_o, lb_attr);
   const long mode = PyLong_AsLong(a[4]);
   const double temp = PyFloat_AsDouble(a[5]), clip = PyFloat_AsDouble(a[6]);
   const uint64_t seed = PyLong_AsUnsignedLongLongMask(a[8]);
@@ -498,21 +544,34 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     if (ain && !fits(*ain, dev, at::kLong, b)) Py_RETURN_NONE;
     // the untouched arange: to_choose[:, 0] == k in every row (k + remaining columns == P)
     const bool uniform = ktc >= 0 && ktc < p && ktc + tc.size(1) == p;
-    const bool in_place = exclusively_held(as_o, asg);
+    const bool asg_here = exclusively_held(as_o, asg);
+    const SlapBlock blk(b, l);
+    bool blk_here = false;
+    if (dn_o && rw_o) {
+      PyObject* const os[4] = {mask_o, i_o, dn_o, rw_o};
+      const at::Tensor* const ts[4] = {&mask, &i, &THPVariable_Unpack(dn_o), &THPVariable_Unpack(rw_o)};
+      blk_here = blk.held_alone(os, ts, b, l);
+    }
     const int64_t kb = up(8 * b);
     const int64_t ko = g_slab.take(dev, 2 * kb);
     at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
     at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b});
-    Carver c;
-    const int64_t om = c.take(b * l), oi = c.take(8 * b), od = c.take(b), orw = c.take(b);
     void* stream = current_stream(dev);
-    const c10::Storage st = g_state.acquire(dev, c.off, stream);
-    at::Tensor asg_out = in_place ? asg : view_of(new_storage(dev, 4 * b * p), at::kInt, 0,
+    at::Tensor asg_out = asg_here ? asg : view_of(new_storage(dev, 4 * b * p), at::kInt, 0,
                                                   asg.sizes());
-    at::Tensor mask_out = view_of(st, at::kBool, om, {b, l});
-    at::Tensor i_out = view_of(st, at::kLong, oi, i.sizes());
-    at::Tensor done = view_of(st, at::kBool, od, {b, 1});
-    at::Tensor reward = view_of(st, at::kBool, orw, {b, 1});
+    at::Tensor mask_out, i_out, done, reward;
+    if (blk_here) {
+      mask_out = mask;
+      i_out = i;
+      done = THPVariable_Unpack(dn_o);
+      reward = THPVariable_Unpack(rw_o);
+    } else {
+      const c10::Storage st = new_storage(dev, blk.nbytes);
+      mask_out = view_of(st, at::kBool, blk.om, {b, l});
+      i_out = view_of(st, at::kLong, blk.oi, {b, 1});
+      done = view_of(st, at::kBool, blk.od, {b, 1});
+      reward = view_of(st, at::kBool, blk.orw, {b, 1});
+    }
     int rc;
     Py_BEGIN_ALLOW_THREADS
     rc = fn(b, l, p, logits.const_data_ptr<float>(), logits.stride(0),
@@ -527,29 +586,50 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
             status.mutable_data_ptr<int32_t>(), stream);
     Py_END_ALLOW_THREADS
     if (rc != CO_OK) return PyLong_FromLong(rc);
-    if (in_place) asg.unsafeGetTensorImpl()->bump_version();  // an in-place write
+    if (asg_here) asg.unsafeGetTensorImpl()->bump_version();  // in-place writes
+    if (blk_here) {
+      mask.unsafeGetTensorImpl()->bump_version();
+      i.unsafeGetTensorImpl()->bump_version();
+      done.unsafeGetTensorImpl()->bump_version();
+      reward.unsafeGetTensorImpl()->bump_version();
+    }
     PyObject* tc_next = THPVariable_Wrap(drop_first_col(tc));  // to_choose[:, 1:]
     if (!tc_next) return nullptr;
-    if (uniform && remember(tc_next, g_attr_tc, ktc + 1)) {
-      Py_DECREF(tc_next);
+    int err = uniform ? remember(tc_next, g_attr_tc, ktc + 1) : 0;
+    if (!err) err = PyDict_SetItemString(td, "to_choose", tc_next);
+    Py_DECREF(tc_next);
+    if (err) return nullptr;
+    PyObject* a_o = THPVariable_Wrap(std::move(act));
+    PyObject* l_o = a_o ? THPVariable_Wrap(std::move(logp)) : nullptr;
+    if (!a_o || !l_o) {
+      Py_XDECREF(a_o);
       return nullptr;
     }
-    PyObject* res = td_finish(td, key, ain_o, act, logp,
-                              {{"assignment", &asg_out}, {"action_mask", &mask_out},
-                               {"i", &i_out}, {"reward", &reward}, {"done", &done}},
-                              {{"to_choose", tc_next}}, i_o, lb_attr, "i");
-    Py_DECREF(tc_next);
-    // i is uniform over the batch when the env knows its value (reset: 0; every step +1)
-    // and done = (i == P-1) then is too: the records let poll_done answer without a read
-    if (res && ki >= 0) {
+    PyObject* sel = ain_o != Py_None ? ain_o : a_o;
+    err = PyDict_SetItem(td, key, sel);
+    if (!err && !asg_here) err = set_wrapped(td, "assignment", asg_out);
+    if (!err && !blk_here) {
+      err = set_wrapped(td, "action_mask", mask_out);
+      if (!err) err = set_wrapped(td, "i", i_out);
+      if (!err) err = set_wrapped(td, "reward", reward);
+      if (!err) err = set_wrapped(td, "done", done);
+    }
+    // records on the new i / done: the done lower bound (lb - 1), and -- i uniform over the
+    // batch when the env knows its value (reset: 0; each step +1) -- i + 1 and done = (i ==
+    // P-1), so poll_done answers without a read
+    if (!err) {
       PyObject* i_n = PyDict_GetItemString(td, "i");
       PyObject* d_n = PyDict_GetItemString(td, "done");
-      if (!i_n || !d_n || remember(i_n, g_attr_i, ki + 1) ||
-          remember(d_n, g_attr_i, ki == p - 1 ? 1 : 0)) {
-        Py_DECREF(res);
-        return nullptr;
+      if (!i_n || !d_n) err = -1;
+      if (!err && lb >= 0) err = remember(i_n, lb_attr, lb > 0 ? lb - 1 : 0);
+      if (!err && ki >= 0) {
+        err = remember(i_n, g_attr_i, ki + 1);
+        if (!err) err = remember(d_n, g_attr_i, ki == p - 1 ? 1 : 0);
       }
     }
+    PyObject* res = err ? nullptr : PyTuple_Pack(2, sel, l_o);
+    Py_DECREF(a_o);
+    Py_DECREF(l_o);
     return res;
   } catch (const std::exception& e) {
     PyErr_SetString(PyExc_RuntimeError, e.what());

@@ -157,6 +157,7 @@ def test_glue_epilogue_routing_tsp_cvrp(dev, env_cls):
     from rl4co_slap_amd.utils import decoding as D
 
     s = D.Greedy()
+    td, env, _ = s.pre_decoder_hook(td, env)
     s.steps_hint = n
     steps = 0
     while not bool(td["done"].all()):
