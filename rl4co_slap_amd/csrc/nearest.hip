@@ -18,6 +18,17 @@ namespace {
 
 constexpr int kNoNode = 0x7fffffff;
 
+#ifndef CO_NEAREST_LDS
+#define CO_NEAREST_LDS 1  // 0: the register engines (coordinates in VGPRs, a visited bit mask)
+#endif
+
+#ifndef CO_NEAREST_LDS_G
+#define CO_NEAREST_LDS_G 4  // TSP N <= 104: lanes per instance (4 x 26 slots, or 8 x 14)
+#endif
+#ifndef CO_NEAREST_CVRP_G
+#define CO_NEAREST_CVRP_G 8  // CVRP N + 1 <= 112: lanes per instance (4 x 28 or 8 x 14 slots)
+#endif
+
 #ifndef CO_NEAREST_G8
 #define CO_NEAREST_G8 0  // 1: 8 lanes x 13 slots per instance for N (+1) <= 104 (payload by shuffle)
 #endif
@@ -408,6 +419,362 @@ inline unsigned group_grid(int64_t B, int G) {  // a wave per 64/G instances, co
   return cover_grid((B * G + 63) / 64, 4);
 }
 
+// ---------------------------------------------------------------------------------------
+// LDS-row episodes (the default engines).  The per-step cost of the register engines above
+// is the per-candidate VALU work: two subtractions, two products, a sum, the visited /
+// capacity bit test and four selects per node.  Here each lane keeps its slots' y (and CVRP
+// demand) in registers as pairs, and the instance's x row lives in LDS, slot pairs
+// (x_k, x_k+1) of its G lanes adjacent; a visited node (and every padding slot, and the CVRP
+// depot) has x = NaN, so its distance is NaN and it can never be the minimum -- visiting is
+// one LDS store instead of a per-candidate test.  Per pair of candidates: one 8-byte LDS
+// read, five packed f32 operations (v_pk_add / v_pk_mul: the same IEEE operations, two
+// slots at a time), and per candidate a key = the squared distance's bits with the low KB
+// bits replaced by the slot (one v_and_or) folded into the lane's two smallest keys
+// (v_med3_u32 + v_min_u32).  The group merges (min, second min) pairs over DPP, and the
+// winner is exact without a sqrt per candidate:
+//   keys compare as (truncated squared distance, node); with T = the squared distance's
+//   bits with the low BB bits cleared (a relative error below 2^(BB-23)), if the second
+//   smallest key's T exceeds the winner's T by a factor 1 + 2^(BB-20), every other
+//   candidate's squared distance is above the winner's by more than a factor
+//   1 + 2^(BB-21), so its correctly rounded sqrt is strictly larger: the winner is the
+//   unique argmin of the rounded distances.  Otherwise (a near tie, a winner below 2^-100
+//   where the relative bound does not hold, or an infinite distance) the wave redoes the
+//   step with the correctly rounded sqrt per candidate and the lowest-index tie break
+//   (lds_exact) -- about once per 10^4 instance-steps on uniform coordinates.
+// The winner's coordinates (and demand) come from the input rows in global memory (L2 /
+// MALL hits, hidden by the other waves): with only x in LDS, 4 B per slot, every wave of a
+// B = 65,536 episode is resident at once (a 13 KB (x, y) row per wave would leave a second,
+// one-third-occupied round of waves).
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+constexpr int clog2(int v) {
+  int b = 0;
+  while ((1 << b) < v) ++b;
+  return b;
+}
+
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// float index of node c's x in its instance's x row: node c is slot c / G of lane c % G,
+// slots in pairs of 8 bytes, a pair's G lanes adjacent
+template <int G>
+__device__ __forceinline__ int lds_xoff(int c) {
+  const unsigned k = (unsigned)c / G, sl = (unsigned)c % G;
+  return (int)(((k >> 1) * G + sl) * 2 + (k & 1));
+}
+
+// the lane's two smallest keys (m1 <= m2) over its EPL slots; DEM: a customer whose demand
+// does not fit (dm + used > vcap, cvrp/env.py:140) gets the key ~0
+template <int G, int EPL, bool DEM>
+__device__ __forceinline__ void lds_scan(const float2* __restrict__ rowx2, int sl, float cx,
+                                         float cy, const v2f (&y2)[EPL / 2],
+                                         const v2f (&dm2)[EPL / 2], float used, float vcap,
+                                         uint32_t& m1, uint32_t& m2) {
+  constexpr uint32_t KM = (1u << clog2(EPL)) - 1u;
+  const v2f cx2 = {cx, cx}, cy2 = {cy, cy};
+  const v2f u2 = {used, used};
+  m1 = 0xffffffffu;
+  m2 = 0xffffffffu;
+#pragma unroll
+  for (int p = 0; p < EPL / 2; ++p) {
+    const float2 q = rowx2[p * G + sl];
+    const v2f x = {q.x, q.y};
+    const v2f dx = x - cx2, dy = y2[p] - cy2;
+    const v2f s = dx * dx + dy * dy;  // -ffp-contract=off: two products and a sum
+    v2f du = {0.f, 0.f};
+    if (DEM) du = dm2[p] + u2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t key = (__float_as_uint(s[h]) & ~KM) | (uint32_t)(2 * p + h);
+      if (DEM && du[h] > vcap) key = 0xffffffffu;
+      m2 = med3u(m1, m2, key);
+      m1 = min(m1, key);
+    }
+  }
+}
+
+#ifndef CO_NEAREST_PAY
+#define CO_NEAREST_PAY 0  // 1: the winner's y from the owner lane's registers (select + shuffle)
+#endif
+
+// y2 slot k (binary select tree over k's bits)
+template <int EPL>
+__device__ __forceinline__ float sel_slot(const v2f (&y2)[EPL / 2], unsigned k) {
+  float v[EPL / 2];
+#pragma unroll
+  for (int p = 0; p < EPL / 2; ++p) v[p] = (k & 1u) ? y2[p][1] : y2[p][0];
+  int n = EPL / 2;
+#pragma unroll
+  for (int bit = 1; bit < 6; ++bit) {
+    if (n <= 1) break;
+#pragma unroll
+    for (int i = 0; i < (n + 1) / 2; ++i)
+      v[i] = (2 * i + 1 < n && ((k >> bit) & 1u)) ? v[2 * i + 1] : v[2 * i];
+    n = (n + 1) / 2;
+  }
+  return v[0];
+}
+
+// (smallest, second smallest) over the group's lanes
+template <int G>
+__device__ __forceinline__ void grp_min2(uint32_t& m1, uint32_t& m2) {
+#define CO_MIN2(C)                                             \
+  {                                                            \
+    const uint32_t t1 = dpp_u<C>(m1), t2 = dpp_u<C>(m2);       \
+    m2 = med3u(m1, t1, min(m2, t2));                           \
+    m1 = min(m1, t1);                                          \
+  }
+  if (G >= 2) CO_MIN2(0xB1);
+  if (G >= 4) CO_MIN2(0x4E);
+  if (G >= 8) CO_MIN2(0x141);
+  if (G >= 16) CO_MIN2(0x140);
+#undef CO_MIN2
+  if (G >= 32) {
+    const auto a = __builtin_amdgcn_permlane16_swap(m1, m1, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(m2, m2, false, false);
+    m2 = med3u(a[0], a[1], min(b[0], b[1]));
+    m1 = min(a[0], a[1]);
+  }
+  if (G >= 64) {
+    const auto a = __builtin_amdgcn_permlane32_swap(m1, m1, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(m2, m2, false, false);
+    m2 = med3u(a[0], a[1], min(b[0], b[1]));
+    m1 = min(a[0], a[1]);
+  }
+}
+
+// The rare exact step: per candidate the correctly rounded f32 distance, the group argmin
+// with the lowest-index tie break (torch.argmin over the oracle's distances); kNoNode when
+// no candidate has a finite distance.
+template <int G, int EPL, bool DEM>
+__device__ __noinline__ int lds_exact(const float* __restrict__ rowx, int sl, float cx, float cy,
+                                      const v2f (&y2)[EPL / 2], const v2f (&dm2)[EPL / 2],
+                                      float used, float vcap) {
+  float best = __builtin_inff();
+  int bi = kNoNode;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const int c = k * G + sl;
+    // NaN for visited / padding: never taken
+    const float d = edge_len(cx, cy, rowx[lds_xoff<G>(c)], y2[k >> 1][k & 1]);
+    const bool fits = !DEM || !(dm2[k >> 1][k & 1] + used > vcap);
+    if (fits && d < best) {
+      best = d;
+      bi = c;
+    }
+  }
+  grp_argmin_split<G>(best, bi);
+  return bi;
+}
+
+// The group's nearest candidate: the node, or kNoNode when every slot is poisoned (no
+// candidate).  Every lane of the wave must take part.
+template <int G, int EPL, bool DEM>
+__device__ __forceinline__ int lds_nearest(const float* __restrict__ rowx, int sl, float cx,
+                                           float cy, const v2f (&y2)[EPL / 2],
+                                           const v2f (&dm2)[EPL / 2], float used, float vcap) {
+  constexpr uint32_t KM = (1u << clog2(EPL)) - 1u, BM = (1u << clog2(G * EPL)) - 1u;
+  constexpr float kWin = 1.0f + (float)(1u << clog2(G * EPL)) * 0x1p-20f;
+  uint32_t m1, m2;
+  lds_scan<G, EPL, DEM>(reinterpret_cast<const float2*>(rowx), sl, cx, cy, y2, dm2, used, vcap,
+                        m1, m2);
+  // lane keys (T | slot) -> group keys (T | node); slot * G + lane < 2^BB never reaches T
+  m1 = (m1 & ~BM) | ((m1 & KM) * G + sl);
+  m2 = (m2 & ~BM) | ((m2 & KM) * G + sl);
+  grp_min2<G>(m1, m2);
+  const uint32_t t1 = m1 & ~BM, t2 = m2 & ~BM;
+  const bool none = t1 >= 0x7fc00000u;  // every slot NaN or ~0
+  const bool ok = none || (t1 >= 0x0d800000u && t1 < 0x7f800000u &&
+                           t2 > __float_as_uint(__uint_as_float(t1) * kWin));
+  int w = none ? kNoNode : (int)(m1 & BM);
+  if (__builtin_expect(__any(!ok), 0))
+    w = lds_exact<G, EPL, DEM>(rowx, sl, cx, cy, y2, dm2, used, vcap);
+  return w;
+}
+
+// TSP with the x rows in LDS (see above): one wave per block, 64/G instances per wave.
+template <int G, int EPL>
+__global__ __launch_bounds__(64) void tsp_nearest_lds_kernel(
+    int64_t B, int N, const float2* __restrict__ locs, int64_t* __restrict__ acts_out,
+    uint8_t* __restrict__ mask_out, int64_t* __restrict__ first_out,
+    int64_t* __restrict__ cur_out, int64_t* __restrict__ i_out, uint8_t* __restrict__ done_out,
+    uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out) {
+  static_assert(EPL % 2 == 0 && (G & (G - 1)) == 0 && G * EPL <= 1024, "slot pairs");
+  constexpr int IPW = 64 / G, SLOTS = G * EPL;
+  __shared__ float2 s_x[IPW * SLOTS / 2];
+  const int lane = threadIdx.x, sl = lane % G, gi = lane / G;
+  const int64_t base = (int64_t)blockIdx.x * IPW;
+  if (base >= B) return;  // block-uniform
+  const int64_t b = base + gi;
+  const bool valid = b < B;
+  const int64_t bb = valid ? b : B - 1;  // a dead group mirrors the last instance
+  const float2* lrow = locs + bb * N;
+  float* const rowx = reinterpret_cast<float*>(s_x) + gi * SLOTS;
+  const float qnan = __builtin_nanf("");
+  v2f y2[EPL / 2];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {  // padding slots: x NaN
+    const int c = k * G + sl;
+    const float2 q = c < N ? lrow[c] : make_float2(qnan, 0.f);
+    rowx[lds_xoff<G>(c)] = q.x;
+    y2[k >> 1][k & 1] = q.y;
+  }
+  const v2f nodem[EPL / 2] = {};  // no demand
+  const float2 q0 = lrow[0];  // step 0: node 0
+  __syncthreads();
+  rowx[0] = qnan;
+  float cx = q0.x, cy = q0.y;
+  if (valid && sl == 0) acts_out[bb] = 0;
+  double len = 0.0;
+  int cur = 0;
+  for (int t = 1; t < N; ++t) {
+    int a = lds_nearest<G, EPL, false>(rowx, sl, cx, cy, y2, nodem, 0.f, 0.f);
+    a = a == kNoNode ? 0 : a;  // only when every remaining distance is infinite
+#if CO_NEAREST_PAY
+    float* px = rowx + lds_xoff<G>(a);
+    const float2 q = make_float2(*px, __shfl(sel_slot<EPL>(y2, (unsigned)a / G), (lane - sl) + a % G, 64));
+    *px = qnan;  // visited
+#else
+    rowx[lds_xoff<G>(a)] = qnan;  // visited
+    const float2 q = lrow[a];
+#endif
+    len += (double)edge_len(cx, cy, q.x, q.y);
+    cx = q.x;
+    cy = q.y;
+    cur = a;
+    if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
+  }
+  len += (double)edge_len(cx, cy, q0.x, q0.y);
+  if (!valid) return;
+  uint8_t* mrow = mask_out + bb * N;
+  for (int c = sl; c < N; c += G) mrow[c] = 0;  // every node visited
+  if (sl == 0) {
+    first_out[bb] = 0;
+    cur_out[bb] = cur;
+    i_out[bb] = N;
+    done_out[bb] = 1;
+    step_reward_out[bb] = 0;
+    reward_out[bb] = -(float)len;
+  }
+}
+
+// CVRP with the x rows in LDS (the depot's x NaN: never a candidate), y and demand per slot
+// in registers (the capacity test, packed), the chosen customer's coordinates and demand
+// from the input rows.  The transition, finishing and final rows are those of
+// cvrp_nearest_episode_kernel; a customer is visited iff its LDS x is NaN (NaN input
+// coordinates would read as visited).
+template <int G, int EPL>
+__global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
+    int64_t B, int N, const float2* __restrict__ depot, const float2* __restrict__ locs_in,
+    const float* __restrict__ demand, float vcap, int max_steps, int64_t* __restrict__ acts_out,
+    float2* __restrict__ locs_out, int64_t* __restrict__ cur_out, float* __restrict__ used_out,
+    float* __restrict__ vcap_out, uint8_t* __restrict__ visited_out,
+    uint8_t* __restrict__ mask_out, uint8_t* __restrict__ done_out,
+    uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out,
+    int32_t* __restrict__ len_out, int32_t* __restrict__ tmax, int32_t* status) {
+  static_assert(EPL % 2 == 0 && (G & (G - 1)) == 0 && G * EPL <= 1024, "slot pairs");
+  constexpr int IPW = 64 / G, SLOTS = G * EPL;
+  __shared__ float2 s_x[IPW * SLOTS / 2];
+  const int lane = threadIdx.x, sl = lane % G, gi = lane / G, gbase = lane - sl;
+  const int M = N + 1;
+  const int64_t base = (int64_t)blockIdx.x * IPW;
+  if (base >= B) return;  // block-uniform
+  const int64_t b = base + gi;
+  const bool valid = b < B;
+  const int64_t bb = valid ? b : B - 1;  // a dead group mirrors the last instance
+  const float2* lrow = locs_in + bb * N;  // customer c >= 1 is lrow[c - 1]
+  const float* drow = demand + bb * N;
+  float* const rowx = reinterpret_cast<float*>(s_x) + gi * SLOTS;
+  const float qnan = __builtin_nanf("");
+  const float2 dep = depot[bb];
+  v2f y2[EPL / 2], dm2[EPL / 2];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const int c = k * G + sl;
+    float2 q = make_float2(qnan, 0.f);
+    float d = 0.f;
+    if (c == 0) {
+      q = dep;
+    } else if (c <= N) {
+      q = lrow[c - 1];
+      d = drow[c - 1];
+    }
+    if (valid && locs_out && c <= N) locs_out[bb * M + c] = q;
+    rowx[lds_xoff<G>(c)] = c == 0 ? qnan : q.x;  // the depot is never a nearest candidate
+    y2[k >> 1][k & 1] = q.y;
+    dm2[k >> 1][k & 1] = d;
+  }
+  __syncthreads();
+  float cx = dep.x, cy = dep.y, used = 0.f;
+  // st = customers visited (bits 0-15) | steps taken (bits 16-30) | depot entered (bit 31)
+  uint32_t st = 0;
+  int cur = 0;
+  bool done = false;
+  double dist = 0.0;
+  for (int t = 0; t < max_steps; ++t) {
+    if (__ballot(!done) == 0) break;  // wave-uniform: the group reductions need every lane
+    const int w = lds_nearest<G, EPL, true>(rowx, sl, cx, cy, y2, dm2, used, vcap);
+    if (done) continue;
+    const int a = w == kNoNode ? 0 : w;
+    float2 q = dep;
+    float ad = 0.f;
+    if (a != 0) {
+      rowx[lds_xoff<G>(a)] = qnan;  // visited
+      q = lrow[a - 1];
+      ad = drow[a - 1];
+    }
+    const float dx = q.x - cx, dy = q.y - cy;
+    dist += (double)__builtin_sqrtf(dx * dx + dy * dy);
+    used = a != 0 ? (used + ad) * 1.0f : 0.0f;  // cvrp/env.py:83-85
+    st = ((st & 0x8000ffffu) + (a != 0 ? 1u : 0u)) | ((uint32_t)(t + 1) << 16) |
+         (a == 0 ? 0x80000000u : 0u);
+    cur = a;
+    cx = q.x;
+    cy = q.y;
+    if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
+    done = (st & 0x8000ffffu) == (0x80000000u | (uint32_t)N);
+  }
+  const int len = (int)((st >> 16) & 0x7fffu);
+  dist += (double)edge_len(cx, cy, dep.x, dep.y);  // closing edge to the depot
+  // final state rows: visited and get_action_mask (cvrp/env.py:137-149)
+  bool any_feas = false;
+  uint8_t* vrow = visited_out + bb * M;
+  uint8_t* mrow = mask_out + bb * M;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const int c = k * G + sl;
+    const bool v = c == 0 ? (st >> 31) != 0 : __builtin_isnan(rowx[lds_xoff<G>(c)]);
+    const bool feas = c >= 1 && c <= N && !v && !(dm2[k >> 1][k & 1] + used > vcap);
+    any_feas |= feas;
+    if (valid && c <= N) {
+      vrow[c] = v;
+      if (c >= 1) mrow[c] = feas;
+    }
+  }
+  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+  const bool anyf = (__ballot(any_feas) & gmask) != 0;
+  if (valid && sl == 0) {
+    mrow[0] = !((cur == 0) && anyf);
+    cur_out[bb] = cur;
+    used_out[bb] = used;
+    vcap_out[bb] = vcap;
+    done_out[bb] = done;
+    step_reward_out[bb] = 0;
+    reward_out[bb] = -(float)dist;
+    len_out[bb] = len;
+    if (!done) set_status(status, CO_ST_TRUNCATED);
+    atomicMax(tmax, len);
+  }
+}
+
+inline unsigned lds_grid(int64_t B, int G) {  // a one-wave block per 64/G instances
+  return cover_grid(B, 64 / G, 64);
+}
+
 }  // namespace
 
 // Called by co_tsp_rollout for the nearest policy (acts_in == NULL).
@@ -423,6 +790,22 @@ int co_internal_tsp_nearest_rollout(int64_t B, int64_t N, const float* locs, int
                      dim3(group_grid(B, G)), dim3(256),                                         \
                      0, s, B, (int)N, l2, acts_out, mask_out, first_out, cur_out, i_out,       \
                      done_out, step_reward_out, reward_out)
+#define CO_TSPL(G, EPL)                                                                        \
+  hipLaunchKernelGGL((tsp_nearest_lds_kernel<G, EPL>), dim3(lds_grid(B, G)), dim3(64), 0, s, B,  \
+                     (int)N, l2, acts_out, mask_out, first_out, cur_out, i_out, done_out,        \
+                     step_reward_out, reward_out)
+  if (CO_NEAREST_LDS) {
+    if (N <= 32) CO_TSPL(4, 8);
+    else if (N <= 64) CO_TSPL(4, 16);
+    else if (N <= 104 && CO_NEAREST_LDS_G == 4) CO_TSPL(4, 26);
+    else if (N <= 112) CO_TSPL(8, 14);
+    else if (N <= 128) CO_TSPL(8, 16);
+    else if (N <= 256) CO_TSPL(8, 32);
+    else if (N <= 512) CO_TSPL(16, 32);
+    else CO_TSPL(32, 32);
+    return launch_status();
+  }
+#undef CO_TSPL
   if (N <= 32) CO_TSPN(4, 8);
   else if (N <= 64) CO_TSPN(8, 8);
   else if (CO_NEAREST_G8 && N <= 104) CO_TSPN(8, 13);
@@ -466,7 +849,20 @@ extern "C" int co_cvrp_rollout(int64_t B, int64_t N, const float* depot, const f
                      cur_out, used_out, vcap_out, visited_out, mask_out, done_out,             \
                      step_reward_out, reward_out, len_out, steps_out, status)
   const int64_t M = N + 1;
-  if (M <= 32) CO_CVRPN(4, 8);
+#define CO_CVRPL(G, EPL)                                                                       \
+  hipLaunchKernelGGL((cvrp_nearest_lds_kernel<G, EPL>), dim3(lds_grid(B, G)), dim3(64), 0, s, B, \
+                     (int)N, d2, l2, demand, vcap, (int)max_steps, acts_out, lo, cur_out,        \
+                     used_out, vcap_out, visited_out, mask_out, done_out, step_reward_out,       \
+                     reward_out, len_out, steps_out, status)
+  if (CO_NEAREST_LDS) {
+    if (M <= 32) CO_CVRPL(4, 8);
+    else if (M <= 64) CO_CVRPL(4, 16);
+    else if (M <= 112) CO_CVRPL(CO_NEAREST_CVRP_G, 112 / CO_NEAREST_CVRP_G);
+    else if (M <= 128) CO_CVRPL(8, 16);
+    else if (M <= 256) CO_CVRPL(8, 32);
+    else if (M <= 512) CO_CVRPL(16, 32);
+    else CO_CVRPL(32, 32);
+  } else if (M <= 32) CO_CVRPN(4, 8);
   else if (M <= 64) CO_CVRPN(8, 8);
   else if (CO_NEAREST_G8 && M <= 104) CO_CVRPN(8, 13);
   else if (M <= 112) CO_CVRPN(16, 7);
@@ -475,6 +871,7 @@ extern "C" int co_cvrp_rollout(int64_t B, int64_t N, const float* depot, const f
   else if (M <= 512) CO_CVRPN(64, 8);
   else CO_CVRPN(64, 16);
 #undef CO_CVRPN
+#undef CO_CVRPL
   hipLaunchKernelGGL(cvrp_pad_kernel, dim3(grid_for(B, 256, 2048)), dim3(256), 0, s, B, len_out,
                      steps_out, acts_out, cur_out, used_out);
   return launch_status();

@@ -18,6 +18,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "co_env.h"
@@ -276,37 +277,53 @@ PyObject* tsp_decode_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
   }
 }
 
+// The td's keys as interned strings, made once per string literal (the literal's address
+// keys the table; every caller passes a literal): a dict lookup by an interned key skips
+// PyDict_GetItemString's string construction and hashing.
+inline PyObject* key_of(const char* s) {
+  static std::unordered_map<const char*, PyObject*> keys;
+  auto it = keys.find(s);
+  if (it != keys.end()) return it->second;
+  PyObject* o = PyUnicode_InternFromString(s);  // kept for the process's life
+  keys.emplace(s, o);
+  return o;
+}
+
 // ---- host-side knowledge on state tensors (envs/base.py) ---------------------------
-// A record (version, value) in a tensor's attribute: valid while the tensor's version
-// counter is unchanged (nobody modified it in place since the env produced it).
+// A record in a tensor's instance dict, one int (version << 32) | value: valid while the
+// tensor's version counter is unchanged (nobody modified it in place since the env
+// produced it).  Read and written straight in the instance dict (no attribute lookup
+// through the type, no tuple), a few tens of ns each.
 PyObject* g_attr_i = nullptr;  // "_co_i": the value every entry of an `i` tensor holds
 PyObject* g_attr_tc = nullptr;  // "_co_tc": to_choose is the env's untouched arange from k on
 
 // the record's value, or -1 (absent / stale)
 long long known(PyObject* t, PyObject* attr) {
-  PyObject* rec = nullptr;
-  if (_PyObject_LookupAttr(t, attr, &rec) <= 0) {
+  PyObject** dp = _PyObject_GetDictPtr(t);
+  if (!dp || !*dp) return -1;
+  PyObject* rec = PyDict_GetItemWithError(*dp, attr);  // borrowed
+  if (!rec || !PyLong_CheckExact(rec)) {
     PyErr_Clear();
     return -1;
   }
-  long long v = -1;
-  if (PyTuple_Check(rec) && PyTuple_GET_SIZE(rec) == 2) {
-    const long long ver = PyLong_AsLongLong(PyTuple_GET_ITEM(rec, 0));
-    if (ver == (long long)THPVariable_Unpack(t)._version())
-      v = PyLong_AsLongLong(PyTuple_GET_ITEM(rec, 1));
-    if (PyErr_Occurred()) {
-      PyErr_Clear();
-      v = -1;
-    }
+  int overflow = 0;
+  const long long r = PyLong_AsLongLongAndOverflow(rec, &overflow);
+  if (overflow || r < 0) {
+    PyErr_Clear();
+    return -1;
   }
-  Py_DECREF(rec);
-  return v;
+  if ((r >> 32) != (long long)THPVariable_Unpack(t)._version()) return -1;
+  return r & 0xffffffffLL;
 }
 
 int remember(PyObject* t, PyObject* attr, long long value) {
-  PyObject* rec = Py_BuildValue("(LL)", (long long)THPVariable_Unpack(t)._version(), value);
+  PyObject** dp = _PyObject_GetDictPtr(t);
+  if (!dp) return PyObject_SetAttr(t, attr, Py_None);  // raises the type's error
+  if (!*dp && !(*dp = PyDict_New())) return -1;
+  const long long ver = (long long)THPVariable_Unpack(t)._version();
+  PyObject* rec = PyLong_FromLongLong((ver << 32) | (value & 0xffffffffLL));
   if (!rec) return -1;
-  const int r = PyObject_SetAttr(t, attr, rec);
+  const int r = PyDict_SetItem(*dp, attr, rec);
   Py_DECREF(rec);
   return r;
 }
@@ -331,13 +348,13 @@ PyObject* tsp_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
       (ain_o != Py_None && !is_tensor(ain_o)) || !PyUnicode_Check(key) ||
       !PyUnicode_Check(lb_attr))
     Py_RETURN_NONE;
-  PyObject* mask_o = PyDict_GetItemString(td, "action_mask");  // borrowed
-  PyObject* i_o = PyDict_GetItemString(td, "i");
+  PyObject* mask_o = PyDict_GetItem(td, key_of("action_mask"));  // borrowed
+  PyObject* i_o = PyDict_GetItem(td, key_of("i"));
   if (!mask_o || !i_o || !is_tensor(mask_o) || !is_tensor(i_o)) Py_RETURN_NONE;
   const long long k = known(i_o, g_attr_i);
   if (k < 0) Py_RETURN_NONE;
   const long take = k == 0 ? 1 : 0;
-  PyObject* first_o = take ? nullptr : PyDict_GetItemString(td, "first_node");
+  PyObject* first_o = take ? nullptr : PyDict_GetItem(td, key_of("first_node"));
   if (!take && (!first_o || !is_tensor(first_o))) Py_RETURN_NONE;
   const auto fn = fn_at<TspDecodeStep>(a[0]);
   const long mode = PyLong_AsLong(a[4]);
@@ -372,12 +389,12 @@ PyObject* tsp_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
   int err = remember(o[3], g_attr_i, k + 1);
   if (!err && lb >= 0) err = remember(o[2], lb_attr, lb > 0 ? lb - 1 : 0);
   if (!err) err = PyDict_SetItem(td, key, sel);
-  if (!err) err = PyDict_SetItemString(td, "first_node", o[4]);
-  if (!err) err = PyDict_SetItemString(td, "current_node", sel);
-  if (!err) err = PyDict_SetItemString(td, "i", o[3]);
-  if (!err) err = PyDict_SetItemString(td, "action_mask", o[2]);
-  if (!err) err = PyDict_SetItemString(td, "reward", o[6]);
-  if (!err) err = PyDict_SetItemString(td, "done", o[5]);
+  if (!err) err = PyDict_SetItem(td, key_of("first_node"), o[4]);
+  if (!err) err = PyDict_SetItem(td, key_of("current_node"), sel);
+  if (!err) err = PyDict_SetItem(td, key_of("i"), o[3]);
+  if (!err) err = PyDict_SetItem(td, key_of("action_mask"), o[2]);
+  if (!err) err = PyDict_SetItem(td, key_of("reward"), o[6]);
+  if (!err) err = PyDict_SetItem(td, key_of("done"), o[5]);
   PyObject* res = err ? nullptr : PyTuple_Pack(2, sel, o[1]);
   for (int j = 0; j < 7; ++j) Py_DECREF(o[j]);
   return res;
@@ -408,12 +425,12 @@ PyObject* td_finish(PyObject* td, PyObject* key, PyObject* ain_o, at::Tensor& ac
     }
     if (lb >= 0 && lb_dst && std::strcmp(kv.first, lb_dst) == 0)
       err = remember(o, lb_attr, lb > 0 ? lb - 1 : 0);
-    if (!err) err = PyDict_SetItemString(td, kv.first, o);
+    if (!err) err = PyDict_SetItem(td, key_of(kv.first), o);
     Py_DECREF(o);
   }
   for (auto& kv : views) {
     if (err) break;
-    err = PyDict_SetItemString(td, kv.first, kv.second);
+    err = PyDict_SetItem(td, key_of(kv.first), kv.second);
   }
   PyObject* res = err ? nullptr : PyTuple_Pack(2, sel, l_o);
   Py_DECREF(a_o);
@@ -422,7 +439,7 @@ PyObject* td_finish(PyObject* td, PyObject* key, PyObject* ain_o, at::Tensor& ac
 }
 
 inline PyObject* td_tensor(PyObject* td, const char* k) {  // borrowed; nullptr if absent
-  PyObject* o = PyDict_GetItemString(td, k);
+  PyObject* o = PyDict_GetItem(td, key_of(k));
   return (o && is_tensor(o)) ? o : nullptr;
 }
 
@@ -430,7 +447,7 @@ inline PyObject* td_tensor(PyObject* td, const char* k) {  // borrowed; nullptr 
 inline int set_wrapped(PyObject* td, const char* k, at::Tensor& t) {
   PyObject* o = THPVariable_Wrap(std::move(t));
   if (!o) return -1;
-  const int err = PyDict_SetItemString(td, k, o);
+  const int err = PyDict_SetItem(td, key_of(k), o);
   Py_DECREF(o);
   return err;
 }
@@ -596,7 +613,7 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     PyObject* tc_next = THPVariable_Wrap(drop_first_col(tc));  // to_choose[:, 1:]
     if (!tc_next) return nullptr;
     int err = uniform ? remember(tc_next, g_attr_tc, ktc + 1) : 0;
-    if (!err) err = PyDict_SetItemString(td, "to_choose", tc_next);
+    if (!err) err = PyDict_SetItem(td, key_of("to_choose"), tc_next);
     Py_DECREF(tc_next);
     if (err) return nullptr;
     PyObject* a_o = THPVariable_Wrap(std::move(act));
@@ -618,8 +635,8 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     // batch when the env knows its value (reset: 0; each step +1) -- i + 1 and done = (i ==
     // P-1), so poll_done answers without a read
     if (!err) {
-      PyObject* i_n = PyDict_GetItemString(td, "i");
-      PyObject* d_n = PyDict_GetItemString(td, "done");
+      PyObject* i_n = PyDict_GetItem(td, key_of("i"));
+      PyObject* d_n = PyDict_GetItem(td, key_of("done"));
       if (!i_n || !d_n) err = -1;
       if (!err && lb >= 0) err = remember(i_n, lb_attr, lb > 0 ? lb - 1 : 0);
       if (!err && ki >= 0) {
@@ -994,7 +1011,7 @@ PyObject* slap_reset_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
       int err = 0;
       if (kv.first[0] == 'i') err = remember(o, g_attr_i, 0) || remember(o, lb_attr, p);
       else if (kv.first[0] == 't' && kv.first[1] == 'o') err = remember(o, g_attr_tc, 0);
-      if (!err) err = PyDict_SetItemString(td, kv.first, o);
+      if (!err) err = PyDict_SetItem(td, key_of(kv.first), o);
       Py_DECREF(o);
       if (err) return nullptr;
     }

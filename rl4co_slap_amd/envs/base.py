@@ -221,17 +221,18 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
 
     # -- i-tracking for the batch-wide `i.all() == 0` test ------------------------
     # (the record lives on the tensor: it dies with it, and an in-place change bumps the
-    # version; csrc/pycall/co_torchstep.cpp reads and writes the same records)
+    # version; one int (version << 32) | value, which csrc/pycall/co_torchstep.cpp reads
+    # and writes in the tensor's instance dict)
     @staticmethod
     def _remember_i(t: torch.Tensor, value: int):
-        t._co_i = (t._version, value)
+        t._co_i = (t._version << 32) | int(value)
 
     @staticmethod
     def _known_i(t: torch.Tensor):
         rec = getattr(t, "_co_i", None)
-        if rec is None or rec[0] != t._version:
+        if rec is None or (rec >> 32) != t._version:
             return None
-        return rec[1]
+        return rec & 0xFFFFFFFF
 
     # -- step outputs -------------------------------------------------------------
     def _out(self, shape, dtype, device, stream):
@@ -248,15 +249,15 @@ class RL4COEnvBase(metaclass=abc.ABCMeta):
 
     # -- done-poll lower bounds ---------------------------------------------------
     def _remember_lb(self, t: torch.Tensor, steps: int):
-        setattr(t, self._lb_attr, (t._version, max(int(steps), 0)))
+        setattr(t, self._lb_attr, (t._version << 32) | max(int(steps), 0))
 
     def _known_lb(self, t) -> Optional[int]:
         if not isinstance(t, torch.Tensor):
             return None
         rec = getattr(t, self._lb_attr, None)
-        if rec is None or rec[0] != t._version:
+        if rec is None or (rec >> 32) != t._version:
             return None
-        return rec[1]
+        return rec & 0xFFFFFFFF
 
     def poll_done(self, td):
         """The decode loop's ``td["done"].all()`` (``constructive/base.py:245``), read on
