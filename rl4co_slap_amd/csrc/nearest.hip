@@ -430,8 +430,8 @@ inline unsigned group_grid(int64_t B, int G) {  // a wave per 64/G instances, co
 // read, five packed f32 operations (v_pk_add / v_pk_mul: the same IEEE operations, two
 // slots at a time), and per candidate a key = the squared distance's bits with the low KB
 // bits replaced by the slot (one v_and_or) folded into the lane's two smallest keys
-// (v_med3_u32 + v_min_u32).  The group merges (min, second min) pairs over DPP, and the
-// winner is exact without a sqrt per candidate:
+// (v_med3_u32 + v_min_u32, two independent chains).  The group merges (min, second min)
+// pairs over DPP, and the winner is exact without a sqrt per candidate:
 //   keys compare as (truncated squared distance, node); with T = the squared distance's
 //   bits with the low BB bits cleared (a relative error below 2^(BB-23)), if the second
 //   smallest key's T exceeds the winner's T by a factor 1 + 2^(BB-20), every other
@@ -441,10 +441,12 @@ inline unsigned group_grid(int64_t B, int G) {  // a wave per 64/G instances, co
 //   where the relative bound does not hold, or an infinite distance) the wave redoes the
 //   step with the correctly rounded sqrt per candidate and the lowest-index tie break
 //   (lds_exact) -- about once per 10^4 instance-steps on uniform coordinates.
-// The winner's coordinates (and demand) come from the input rows in global memory (L2 /
-// MALL hits, hidden by the other waves): with only x in LDS, 4 B per slot, every wave of a
-// B = 65,536 episode is resident at once (a 13 KB (x, y) row per wave would leave a second,
-// one-third-occupied round of waves).
+// Nothing is read from global memory inside the step loop: the winner's x comes from the
+// LDS row (before its visit mark), its y from the owner lane's registers (a select tree
+// over the slot's bits, then one lane shuffle), the CVRP demand from a read-only LDS row.
+// The kernels are bound by each wave's dependent-instruction latency (4 waves per SIMD:
+// every wave of a B = 65,536 episode is resident at once with 4 B of LDS per TSP node), so
+// the step's tour-length sqrt is taken one step late, where it overlaps the next scan.
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 constexpr int clog2(int v) {
@@ -467,23 +469,31 @@ __device__ __forceinline__ int lds_xoff(int c) {
   return (int)(((k >> 1) * G + sl) * 2 + (k & 1));
 }
 
+// the lane's x slot pairs from its instance's LDS row
+template <int G, int EPL>
+__device__ __forceinline__ void lds_load_x(const float* __restrict__ rowx, int sl,
+                                           v2f (&x2)[EPL / 2]) {
+  const float2* r2 = reinterpret_cast<const float2*>(rowx);
+#pragma unroll
+  for (int p = 0; p < EPL / 2; ++p) {
+    const float2 q = r2[p * G + sl];
+    x2[p] = (v2f){q.x, q.y};
+  }
+}
+
 // the lane's two smallest keys (m1 <= m2) over its EPL slots; DEM: a customer whose demand
 // does not fit (dm + used > vcap, cvrp/env.py:140) gets the key ~0
 template <int G, int EPL, bool DEM>
-__device__ __forceinline__ void lds_scan(const float2* __restrict__ rowx2, int sl, float cx,
-                                         float cy, const v2f (&y2)[EPL / 2],
-                                         const v2f (&dm2)[EPL / 2], float used, float vcap,
-                                         uint32_t& m1, uint32_t& m2) {
+__device__ __forceinline__ void lds_scan(const v2f (&x2)[EPL / 2], float cx, float cy,
+                                         const v2f (&y2)[EPL / 2], const v2f (&dm2)[EPL / 2],
+                                         float used, float vcap, uint32_t& m1, uint32_t& m2) {
   constexpr uint32_t KM = (1u << clog2(EPL)) - 1u;
   const v2f cx2 = {cx, cx}, cy2 = {cy, cy};
   const v2f u2 = {used, used};
-  m1 = 0xffffffffu;
-  m2 = 0xffffffffu;
+  uint32_t a1 = 0xffffffffu, a2 = 0xffffffffu, b1 = 0xffffffffu, b2 = 0xffffffffu;
 #pragma unroll
   for (int p = 0; p < EPL / 2; ++p) {
-    const float2 q = rowx2[p * G + sl];
-    const v2f x = {q.x, q.y};
-    const v2f dx = x - cx2, dy = y2[p] - cy2;
+    const v2f dx = x2[p] - cx2, dy = y2[p] - cy2;
     const v2f s = dx * dx + dy * dy;  // -ffp-contract=off: two products and a sum
     v2f du = {0.f, 0.f};
     if (DEM) du = dm2[p] + u2;
@@ -491,32 +501,17 @@ __device__ __forceinline__ void lds_scan(const float2* __restrict__ rowx2, int s
     for (int h = 0; h < 2; ++h) {
       uint32_t key = (__float_as_uint(s[h]) & ~KM) | (uint32_t)(2 * p + h);
       if (DEM && du[h] > vcap) key = 0xffffffffu;
-      m2 = med3u(m1, m2, key);
-      m1 = min(m1, key);
+      if (p & 1) {  // two independent (min, second min) chains
+        b2 = med3u(b1, b2, key);
+        b1 = min(b1, key);
+      } else {
+        a2 = med3u(a1, a2, key);
+        a1 = min(a1, key);
+      }
     }
   }
-}
-
-#ifndef CO_NEAREST_PAY
-#define CO_NEAREST_PAY 0  // 1: the winner's y from the owner lane's registers (select + shuffle)
-#endif
-
-// y2 slot k (binary select tree over k's bits)
-template <int EPL>
-__device__ __forceinline__ float sel_slot(const v2f (&y2)[EPL / 2], unsigned k) {
-  float v[EPL / 2];
-#pragma unroll
-  for (int p = 0; p < EPL / 2; ++p) v[p] = (k & 1u) ? y2[p][1] : y2[p][0];
-  int n = EPL / 2;
-#pragma unroll
-  for (int bit = 1; bit < 6; ++bit) {
-    if (n <= 1) break;
-#pragma unroll
-    for (int i = 0; i < (n + 1) / 2; ++i)
-      v[i] = (2 * i + 1 < n && ((k >> bit) & 1u)) ? v[2 * i + 1] : v[2 * i];
-    n = (n + 1) / 2;
-  }
-  return v[0];
+  m1 = min(a1, b1);
+  m2 = med3u(a1, b1, min(a2, b2));
 }
 
 // (smallest, second smallest) over the group's lanes
@@ -549,19 +544,23 @@ __device__ __forceinline__ void grp_min2(uint32_t& m1, uint32_t& m2) {
 
 // The rare exact step: per candidate the correctly rounded f32 distance, the group argmin
 // with the lowest-index tie break (torch.argmin over the oracle's distances); kNoNode when
-// no candidate has a finite distance.
+// no candidate has a finite distance.  A call taking only scalars and pointers (y and the
+// demand re-read from the input rows): passing the register arrays would put them in
+// scratch memory, whose per-wave reservation caps the resident waves.
 template <int G, int EPL, bool DEM>
-__device__ __noinline__ int lds_exact(const float* __restrict__ rowx, int sl, float cx, float cy,
-                                      const v2f (&y2)[EPL / 2], const v2f (&dm2)[EPL / 2],
-                                      float used, float vcap) {
+__device__ __noinline__ int lds_exact(const float* __restrict__ rowx,
+                                      const float2* __restrict__ lrow,
+                                      const float* __restrict__ drow, int lo, int hi, int sl,
+                                      float cx, float cy, float used, float vcap) {
   float best = __builtin_inff();
   int bi = kNoNode;
-#pragma unroll
+#pragma unroll 2
   for (int k = 0; k < EPL; ++k) {
     const int c = k * G + sl;
-    // NaN for visited / padding: never taken
-    const float d = edge_len(cx, cy, rowx[lds_xoff<G>(c)], y2[k >> 1][k & 1]);
-    const bool fits = !DEM || !(dm2[k >> 1][k & 1] + used > vcap);
+    const int ci = c < lo ? 0 : (c > hi ? hi - lo : c - lo);  // in range; x is NaN outside
+    // NaN for visited / padding / the CVRP depot: never taken
+    const float d = edge_len(cx, cy, rowx[lds_xoff<G>(c)], lrow[ci].y);
+    const bool fits = !DEM || !(drow[ci] + used > vcap);
     if (fits && d < best) {
       best = d;
       bi = c;
@@ -574,14 +573,16 @@ __device__ __noinline__ int lds_exact(const float* __restrict__ rowx, int sl, fl
 // The group's nearest candidate: the node, or kNoNode when every slot is poisoned (no
 // candidate).  Every lane of the wave must take part.
 template <int G, int EPL, bool DEM>
-__device__ __forceinline__ int lds_nearest(const float* __restrict__ rowx, int sl, float cx,
-                                           float cy, const v2f (&y2)[EPL / 2],
-                                           const v2f (&dm2)[EPL / 2], float used, float vcap) {
+__device__ __forceinline__ int lds_nearest(const float* __restrict__ rowx,
+                                           const v2f (&x2)[EPL / 2], int sl, float cx, float cy,
+                                           const v2f (&y2)[EPL / 2], const v2f (&dm2)[EPL / 2],
+                                           float used, float vcap,
+                                           const float2* __restrict__ lrow,
+                                           const float* __restrict__ drow, int lo, int hi) {
   constexpr uint32_t KM = (1u << clog2(EPL)) - 1u, BM = (1u << clog2(G * EPL)) - 1u;
   constexpr float kWin = 1.0f + (float)(1u << clog2(G * EPL)) * 0x1p-20f;
   uint32_t m1, m2;
-  lds_scan<G, EPL, DEM>(reinterpret_cast<const float2*>(rowx), sl, cx, cy, y2, dm2, used, vcap,
-                        m1, m2);
+  lds_scan<G, EPL, DEM>(x2, cx, cy, y2, dm2, used, vcap, m1, m2);
   // lane keys (T | slot) -> group keys (T | node); slot * G + lane < 2^BB never reaches T
   m1 = (m1 & ~BM) | ((m1 & KM) * G + sl);
   m2 = (m2 & ~BM) | ((m2 & KM) * G + sl);
@@ -592,9 +593,66 @@ __device__ __forceinline__ int lds_nearest(const float* __restrict__ rowx, int s
                            t2 > __float_as_uint(__uint_as_float(t1) * kWin));
   int w = none ? kNoNode : (int)(m1 & BM);
   if (__builtin_expect(__any(!ok), 0))
-    w = lds_exact<G, EPL, DEM>(rowx, sl, cx, cy, y2, dm2, used, vcap);
+    w = lds_exact<G, EPL, DEM>(rowx, lrow, drow, lo, hi, sl, cx, cy, used, vcap);
   return w;
 }
+
+// (m & x) | (~m & y), opaque to the optimizer (which would otherwise fold the select tree
+// below back into an indexed read and lower that as a compare chain per element)
+__device__ __forceinline__ float bfi(uint32_t m, float x, float y) {
+  float r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(x), "v"(y));
+  return r;
+}
+
+// slot k's value among the lane's pairs: a select tree over k's bits (one v_bfi per node)
+template <int P>
+__device__ __forceinline__ float sel_pair(const v2f (&v)[P], unsigned k) {
+  float t[P];
+  const uint32_t m0 = 0u - (k & 1u);
+#pragma unroll
+  for (int p = 0; p < P; ++p) t[p] = bfi(m0, v[p][1], v[p][0]);
+#pragma unroll
+  for (int w = 1, l = 1; w < P; w <<= 1, ++l) {
+    const uint32_t m = 0u - ((k >> l) & 1u);
+#pragma unroll
+    for (int i = 0; i + w < P; i += 2 * w) t[i] = bfi(m, t[i + w], t[i]);
+  }
+  return t[0];
+}
+
+// the winner's y: its owner lane's register, handed to the group by one lane shuffle
+template <int G, int EPL>
+__device__ __forceinline__ float owner_y(const v2f (&y2)[EPL / 2], int w, int gbase) {
+  const float yv = sel_pair<EPL / 2>(y2, (unsigned)w / G);
+  return __shfl(yv, gbase + w % G, 64);
+}
+
+#ifndef CO_NEAREST_PAY
+#define CO_NEAREST_PAY 0  // the winner's y: 0 from the input row, 1 from the owner lane (tree)
+#endif
+
+// The tour terms sqrtf(sq_t) (correctly rounded, as torch's) summed in f64, G at a time:
+// lane (t mod G) of the group holds step t's squared length until each of the group's G
+// lanes holds one, then every lane takes one sqrt -- a sqrt per G steps instead of one per
+// step.  The lanes' partial sums are added at the end: a sum of f32 terms in f64 is exact
+// while the terms span less than 2^29, so the order does not show in the f32 reward.
+template <int G>
+struct TermAcc {
+  double sum = 0.0;
+  float hold = 0.f;
+  __device__ __forceinline__ void add(float sq, int t, int sl) {
+    const int r = t & (G - 1);  // wave-uniform
+    hold = sl == r ? sq : hold;
+    if (r == G - 1) {
+      sum += (double)__builtin_sqrtf(hold);
+      hold = 0.f;
+    }
+  }
+  __device__ __forceinline__ double total() {  // every lane of the wave
+    return grp_sum_f64<G>(sum + (double)__builtin_sqrtf(hold));
+  }
+};
 
 // TSP with the x rows in LDS (see above): one wave per block, 64/G instances per wave.
 template <int G, int EPL>
@@ -606,7 +664,7 @@ __global__ __launch_bounds__(64) void tsp_nearest_lds_kernel(
   static_assert(EPL % 2 == 0 && (G & (G - 1)) == 0 && G * EPL <= 1024, "slot pairs");
   constexpr int IPW = 64 / G, SLOTS = G * EPL;
   __shared__ float2 s_x[IPW * SLOTS / 2];
-  const int lane = threadIdx.x, sl = lane % G, gi = lane / G;
+  const int lane = threadIdx.x, sl = lane % G, gi = lane / G, gbase = lane - sl;
   const int64_t base = (int64_t)blockIdx.x * IPW;
   if (base >= B) return;  // block-uniform
   const int64_t b = base + gi;
@@ -617,11 +675,11 @@ __global__ __launch_bounds__(64) void tsp_nearest_lds_kernel(
   const float qnan = __builtin_nanf("");
   v2f y2[EPL / 2];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) {  // padding slots: x NaN
+  for (int k = 0; k < EPL; ++k) {  // padding slots: x NaN (loads unconditional: no serial waits)
     const int c = k * G + sl;
-    const float2 q = c < N ? lrow[c] : make_float2(qnan, 0.f);
-    rowx[lds_xoff<G>(c)] = q.x;
-    y2[k >> 1][k & 1] = q.y;
+    const float2 q = lrow[c < N ? c : N - 1];
+    rowx[lds_xoff<G>(c)] = c < N ? q.x : qnan;
+    y2[k >> 1][k & 1] = c < N ? q.y : 0.f;
   }
   const v2f nodem[EPL / 2] = {};  // no demand
   const float2 q0 = lrow[0];  // step 0: node 0
@@ -629,26 +687,33 @@ __global__ __launch_bounds__(64) void tsp_nearest_lds_kernel(
   rowx[0] = qnan;
   float cx = q0.x, cy = q0.y;
   if (valid && sl == 0) acts_out[bb] = 0;
-  double len = 0.0;
+  TermAcc<G> len;
   int cur = 0;
+  v2f x2[EPL / 2];
+  lds_load_x<G, EPL>(rowx, sl, x2);
   for (int t = 1; t < N; ++t) {
-    int a = lds_nearest<G, EPL, false>(rowx, sl, cx, cy, y2, nodem, 0.f, 0.f);
+    int a = lds_nearest<G, EPL, false>(rowx, x2, sl, cx, cy, y2, nodem, 0.f, 0.f, lrow,
+                                       nullptr, 0, N - 1);
     a = a == kNoNode ? 0 : a;  // only when every remaining distance is infinite
-#if CO_NEAREST_PAY
     float* px = rowx + lds_xoff<G>(a);
-    const float2 q = make_float2(*px, __shfl(sel_slot<EPL>(y2, (unsigned)a / G), (lane - sl) + a % G, 64));
-    *px = qnan;  // visited
+#if CO_NEAREST_PAY
+    const float wx = *px, wy = owner_y<G, EPL>(y2, a, gbase);
 #else
-    rowx[lds_xoff<G>(a)] = qnan;  // visited
-    const float2 q = lrow[a];
+    const float2 wq = lrow[a];
+    const float wx = wq.x, wy = wq.y;
 #endif
-    len += (double)edge_len(cx, cy, q.x, q.y);
-    cx = q.x;
-    cy = q.y;
+    *px = qnan;  // visited
+    lds_load_x<G, EPL>(rowx, sl, x2);  // the next step's x pairs
+    const float dx = wx - cx, dy = wy - cy;
+    len.add(dx * dx + dy * dy, t, sl);
+    cx = wx;
+    cy = wy;
     cur = a;
     if (valid && sl == 0) acts_out[(int64_t)t * B + bb] = a;
   }
-  len += (double)edge_len(cx, cy, q0.x, q0.y);
+  const float ex = q0.x - cx, ey = q0.y - cy;  // the closing edge
+  len.add(ex * ex + ey * ey, N, sl);
+  const double tour = len.total();
   if (!valid) return;
   uint8_t* mrow = mask_out + bb * N;
   for (int c = sl; c < N; c += G) mrow[c] = 0;  // every node visited
@@ -658,13 +723,13 @@ __global__ __launch_bounds__(64) void tsp_nearest_lds_kernel(
     i_out[bb] = N;
     done_out[bb] = 1;
     step_reward_out[bb] = 0;
-    reward_out[bb] = -(float)len;
+    reward_out[bb] = -(float)tour;
   }
 }
 
 // CVRP with the x rows in LDS (the depot's x NaN: never a candidate), y and demand per slot
-// in registers (the capacity test, packed), the chosen customer's coordinates and demand
-// from the input rows.  The transition, finishing and final rows are those of
+// in registers (the capacity test, packed), the demand also in a read-only LDS row (the
+// chosen customer's).  The transition, finishing and final rows are those of
 // cvrp_nearest_episode_kernel; a customer is visited iff its LDS x is NaN (NaN input
 // coordinates would read as visited).
 template <int G, int EPL>
@@ -679,6 +744,7 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
   static_assert(EPL % 2 == 0 && (G & (G - 1)) == 0 && G * EPL <= 1024, "slot pairs");
   constexpr int IPW = 64 / G, SLOTS = G * EPL;
   __shared__ float2 s_x[IPW * SLOTS / 2];
+  __shared__ float s_dem[IPW * SLOTS];
   const int lane = threadIdx.x, sl = lane % G, gi = lane / G, gbase = lane - sl;
   const int M = N + 1;
   const int64_t base = (int64_t)blockIdx.x * IPW;
@@ -689,22 +755,21 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
   const float2* lrow = locs_in + bb * N;  // customer c >= 1 is lrow[c - 1]
   const float* drow = demand + bb * N;
   float* const rowx = reinterpret_cast<float*>(s_x) + gi * SLOTS;
+  float* const rowd = s_dem + gi * SLOTS;  // node-indexed
   const float qnan = __builtin_nanf("");
   const float2 dep = depot[bb];
   v2f y2[EPL / 2], dm2[EPL / 2];
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) {
+  for (int k = 0; k < EPL; ++k) {  // loads unconditional (clamped): no serial waits
     const int c = k * G + sl;
-    float2 q = make_float2(qnan, 0.f);
-    float d = 0.f;
-    if (c == 0) {
-      q = dep;
-    } else if (c <= N) {
-      q = lrow[c - 1];
-      d = drow[c - 1];
-    }
+    const int ci = c < 1 ? 0 : (c <= N ? c - 1 : N - 1);
+    const float2 lq = lrow[ci];
+    const float ld = drow[ci];
+    const float2 q = c == 0 ? dep : (c <= N ? lq : make_float2(qnan, 0.f));
+    const float d = (c >= 1 && c <= N) ? ld : 0.f;
     if (valid && locs_out && c <= N) locs_out[bb * M + c] = q;
     rowx[lds_xoff<G>(c)] = c == 0 ? qnan : q.x;  // the depot is never a nearest candidate
+    rowd[c] = d;
     y2[k >> 1][k & 1] = q.y;
     dm2[k >> 1][k & 1] = d;
   }
@@ -714,22 +779,30 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
   uint32_t st = 0;
   int cur = 0;
   bool done = false;
-  double dist = 0.0;
-  for (int t = 0; t < max_steps; ++t) {
+  TermAcc<G> dist;
+  v2f x2[EPL / 2];
+  lds_load_x<G, EPL>(rowx, sl, x2);
+  int t = 0;
+  for (; t < max_steps; ++t) {
     if (__ballot(!done) == 0) break;  // wave-uniform: the group reductions need every lane
-    const int w = lds_nearest<G, EPL, true>(rowx, sl, cx, cy, y2, dm2, used, vcap);
-    if (done) continue;
+    const int w = lds_nearest<G, EPL, true>(rowx, x2, sl, cx, cy, y2, dm2, used, vcap, lrow,
+                                            drow, 1, N);
     const int a = w == kNoNode ? 0 : w;
-    float2 q = dep;
-    float ad = 0.f;
-    if (a != 0) {
-      rowx[lds_xoff<G>(a)] = qnan;  // visited
-      q = lrow[a - 1];
-      ad = drow[a - 1];
-    }
+    float* px = rowx + lds_xoff<G>(a);
+#if CO_NEAREST_PAY
+    const float wx = *px, wy = owner_y<G, EPL>(y2, a, gbase), wd = rowd[a];
+#else
+    const int ai = a == 0 ? 0 : a - 1;
+    const float2 wq = lrow[ai];
+    const float wx = wq.x, wy = wq.y, wd = drow[ai];
+#endif
+    if (!done && a != 0) *px = qnan;  // visited
+    lds_load_x<G, EPL>(rowx, sl, x2);  // the next step's x pairs
+    const float2 q = a == 0 ? dep : make_float2(wx, wy);
     const float dx = q.x - cx, dy = q.y - cy;
-    dist += (double)__builtin_sqrtf(dx * dx + dy * dy);
-    used = a != 0 ? (used + ad) * 1.0f : 0.0f;  // cvrp/env.py:83-85
+    dist.add(done ? 0.f : dx * dx + dy * dy, t, sl);
+    if (done) continue;
+    used = a != 0 ? (used + wd) * 1.0f : 0.0f;  // cvrp/env.py:83-85
     st = ((st & 0x8000ffffu) + (a != 0 ? 1u : 0u)) | ((uint32_t)(t + 1) << 16) |
          (a == 0 ? 0x80000000u : 0u);
     cur = a;
@@ -739,7 +812,9 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
     done = (st & 0x8000ffffu) == (0x80000000u | (uint32_t)N);
   }
   const int len = (int)((st >> 16) & 0x7fffu);
-  dist += (double)edge_len(cx, cy, dep.x, dep.y);  // closing edge to the depot
+  const float ex = dep.x - cx, ey = dep.y - cy;  // the closing edge to the depot
+  dist.add(ex * ex + ey * ey, t, sl);
+  const double tour = dist.total();
   // final state rows: visited and get_action_mask (cvrp/env.py:137-149)
   bool any_feas = false;
   uint8_t* vrow = visited_out + bb * M;
@@ -764,7 +839,7 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
     vcap_out[bb] = vcap;
     done_out[bb] = done;
     step_reward_out[bb] = 0;
-    reward_out[bb] = -(float)dist;
+    reward_out[bb] = -(float)tour;
     len_out[bb] = len;
     if (!done) set_status(status, CO_ST_TRUNCATED);
     atomicMax(tmax, len);

@@ -451,3 +451,56 @@ def test_cvrp_nearest_sqrt_tie(dev, n, same_lane):
     ep.run_eager()
     torch.cuda.synchronize()
     _check_cvrp(ep.final_state(), a, r, tdf)
+
+
+@pytest.mark.parametrize("n", [30, 100, 110])
+@pytest.mark.parametrize("grid", [4, 16])
+def test_nearest_on_a_grid_many_ties(dev, n, grid):
+    """Coordinates on a coarse grid: exact duplicates and many equal distances every step,
+    so the truncated-key ratio test sends most steps down the exact path (lowest index of
+    the rounded-distance minimum) -- TSP and CVRP against the oracle's argmin."""
+    from oracle.envs import CVRPOracle, cvrp_nearest_action
+    from oracle.td import TD
+    from rl4co_slap_amd.rollout.engine import CVRPFusedEpisode
+
+    b = 24
+    g = torch.Generator().manual_seed(n * grid)
+    locs = torch.randint(0, grid, (b, n, 2), generator=g).float() / grid
+    env = TSPOracle(num_loc=n, seed=1)
+    r, tdf, a = ref_rollout(env, env.reset(TD({"locs": locs.clone()}, [b])), tsp_nearest_action)
+    ep = TSPFusedEpisode(locs.to(dev), None, policy="nearest")
+    ep.run_eager()
+    torch.cuda.synchronize()
+    _check(ep.final_state(), a, r, tdf)
+    cenv = CVRPOracle(num_loc=n, seed=3)
+    gen = cenv.generate([b])
+    gen["depot"] = torch.randint(0, grid, (b, 2), generator=g).float() / grid
+    gen["locs"] = torch.randint(0, grid, (b, n, 2), generator=g).float() / grid
+    r, tdf, a = ref_rollout(cenv, cenv.reset(TD({k: v.clone() for k, v in gen.items()}, [b])),
+                            cvrp_nearest_action)
+    ep = CVRPFusedEpisode({k: v.to(dev) for k, v in gen.items()},
+                          vehicle_capacity=float(cenv.vehicle_capacity))
+    ep.run_eager()
+    torch.cuda.synchronize()
+    _check_cvrp(ep.final_state(), a, r, tdf)
+
+
+@pytest.mark.parametrize("scale", [1e-3, 1e-19, 1e-21])
+def test_nearest_tiny_and_near_ratio_distances(dev, scale):
+    """Clusters of points a few `scale` apart (squared distances down to the f32 subnormal
+    range, where the ratio bound does not hold and the exact path runs) and pairs whose
+    squared distances differ by a relative 1e-6 (inside the ratio window, distinct sqrt)."""
+    from oracle.td import TD
+
+    b, n = 16, 100
+    g = torch.Generator().manual_seed(int(-torch.log10(torch.tensor(scale)).item()))
+    centers = torch.rand(b, 10, 2, generator=g) * (1.0 if scale > 1e-6 else scale * 100)
+    locs = (centers.repeat_interleave(10, dim=1)
+            + torch.randint(-3, 4, (b, n, 2), generator=g).float() * scale)
+    locs[:, 1::7] = locs[:, 0:1] + (locs[:, 1::7] - locs[:, 0:1]) * (1 + 1e-6)
+    env = TSPOracle(num_loc=n, seed=1)
+    r, tdf, a = ref_rollout(env, env.reset(TD({"locs": locs.clone()}, [b])), tsp_nearest_action)
+    ep = TSPFusedEpisode(locs.to(dev), None, policy="nearest")
+    ep.run_eager()
+    torch.cuda.synchronize()
+    _check(ep.final_state(), a, r, tdf)
