@@ -29,14 +29,32 @@ namespace {
 // set the kernel's VGPR count, as in co_tsp_decode_step.  The decode's wait for its logits
 // (vmcnt counts in issue order) also covers the DMA; the transition reads the stage after
 // an explicit drain + wave barrier.
+// Whole 64-lane pieces carry no per-lane predicate (a branch per DMA instruction cost more
+// VALU / SALU than the copy itself); only the tail piece masks lanes.
 template <class F>
 __device__ __forceinline__ void dma_dwords(int n, uint32_t* lds_dst, F src) {
   const int lane = lane_id();
-  for (int base = 0; base < n; base += 64) {  // wave-uniform trip count
-    const int k = base + lane;
-    if (k < n)
-      __builtin_amdgcn_global_load_lds((const void*)src(k), (lds_void*)(lds_dst + base), 4, 0, 0);
-  }
+  int base = 0;
+  for (; base + 64 <= n; base += 64)  // wave-uniform trip count
+    __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + base), 4,
+                                     0, 0);
+  if (base < n && lane < n - base)
+    __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + base), 4,
+                                     0, 0);
+}
+
+// n4 16-byte units (src(k): the k-th, 16-byte aligned) to a 16-byte aligned LDS destination:
+// gfx950's global_load_lds_dwordx4, a quarter of the instructions of dma_dwords
+template <class F>
+__device__ __forceinline__ void dma_dwordx4(int n4, uint32_t* lds_dst, F src) {
+  const int lane = lane_id();
+  int base = 0;
+  for (; base + 64 <= n4; base += 64)
+    __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + 4 * base),
+                                     16, 0, 0);
+  if (base < n4 && lane < n4 - base)
+    __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + 4 * base),
+                                     16, 0, 0);
 }
 
 __device__ __forceinline__ void stage_ready() {
@@ -240,13 +258,14 @@ struct CvrpEpi {
   float* ll_accum;
 };
 
-// Per wave (RPW rows): [demand: RPW*N][visited bytes: RPW*(N+1) rounded up to dwords]
+// Per wave (RPW rows; the stage padded to 16 bytes, so a 16-byte aligned demand block
+// comes in by dwordx4): [demand: RPW*N][visited bytes: RPW*(N+1) rounded up to dwords]
 // [used: RPW][capacity: RPW][ll: RPW].  The visited rows of a wave are one contiguous,
 // 4-byte-aligned byte range (the launcher requires RPW*(N+1) % 4 == 0 and an aligned
 // buffer), fetched as whole dwords; the last partial wave's trailing bytes (< 4) by bytes.
 __host__ __device__ inline int cvrp_vis_dwords(int rpw, int N) { return (rpw * (N + 1) + 3) / 4; }
-__host__ __device__ inline int cvrp_stage_dwords(int rpw, int N) {
-  return rpw * N + cvrp_vis_dwords(rpw, N) + 3 * rpw;
+__host__ __device__ inline int cvrp_stage_dwords(int rpw, int N) {  // 16-byte multiple
+  return (rpw * N + cvrp_vis_dwords(rpw, N) + 3 * rpw + 3) & ~3;
 }
 
 template <int RL, int EPL>
@@ -260,7 +279,15 @@ struct CvrpStage {
 
   __device__ __forceinline__ void issue(const CvrpEpi& e, int64_t base, int nr) const {
     const int Nn = N, NC = N + 1;
-    dma_dwords(nr * Nn, dem(), [&](int k) { return e.demand + base * Nn + k; });
+    const float* dsrc = e.demand + base * Nn;
+    const int nd = nr * Nn;
+    if ((reinterpret_cast<uintptr_t>(dsrc) & 15) == 0) {  // wave-uniform
+      const int n4 = nd >> 2;
+      dma_dwordx4(n4, dem(), [&](int k) { return dsrc + 4 * k; });
+      dma_dwords(nd & 3, dem() + 4 * n4, [&](int k) { return dsrc + 4 * n4 + k; });
+    } else {
+      dma_dwords(nd, dem(), [&](int k) { return dsrc + k; });
+    }
     const uint8_t* vrow = e.vis_in + base * NC;
     const int nvb = nr * NC, nvw = nvb >> 2;
     dma_dwords(nvw, vis(), [&](int k) { return reinterpret_cast<const uint32_t*>(vrow) + k; });
