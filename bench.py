@@ -660,7 +660,7 @@ def summarize(out):
                     "host_us_per_loop_step_b64": r(m.get("host_us_per_loop_step_b64"), 2),
                     "decode_fused_kernel_us": r(m.get("decode_fused_kernel_us"), 2),
                     "hbm_frac": r(m.get("hbm_frac"))}
-    for name in ("pomo_tsp100", "cvrp_fused_nearest", "cvrp_stepwise_graph"):
+    for name in ("pomo_tsp100", "tsp_fused_nearest", "cvrp_fused_nearest", "cvrp_stepwise_graph"):
         m = modes.get(name)
         if m:
             sm[name] = {"env_steps_s": r(m["value"], 0), "ms_per_episode": r(m["ms_per_episode"]),
@@ -763,15 +763,19 @@ def annotate_modes(modes, n, world):
             gbs = m["value"] / world * byts / 1e9
             m.update({"alg_bytes_per_env_step": byts, "achieved_GBps_per_gpu": gbs,
                       "hbm_frac": gbs / HBM_PEAK_GBS, "bound": "hbm"})
-    # the in-kernel nearest policies are O(N^2) vector ALU work on register-resident
+    # the in-kernel nearest policies are O(N^2) vector ALU work on LDS / register-resident
     # coordinates, not HBM traffic: per env-step one squared distance
     # per candidate (2 sub + 2 mul + 1 add = 5 FLOP), against the 157.3 TFLOP/s FP32
-    # vector peak (MI355X_MICROARCH.md)
+    # vector peak (MI355X_MICROARCH.md).  The FLOP fraction is small because the bound is
+    # VALU *issue*: the key / min / second-min bookkeeping (3 integer ops per candidate)
+    # and the per-step group reduction are instructions too, and a wave64 instruction takes
+    # ~5 SIMD cycles at 4 waves per SIMD (tools/valu_rates.py); DESIGN.md section 4 counts
+    # the instructions per instance-step.
     for name, cand in (("tsp_fused_nearest", n), ("cvrp_fused_nearest", n + 1)):
         if name in modes and "value" in modes[name]:
             m = modes[name]
             tf = m["value"] / world * cand * 5 / 1e12
-            m.update({"bound": "valu (O(N^2) distance scans, serial step chain)",
+            m.update({"bound": "valu-issue (instructions per instance-step; not HBM)",
                       "achieved_TFLOPs_per_gpu": tf, "valu_frac": tf / FP32_VECTOR_PEAK_TFS})
 
 
@@ -950,10 +954,11 @@ def tsp_decode_step_kernel_us(b, n, dev, reps=50):
 def bench_dropin_cvrp(b, n, k, world, rank, dev):
     """The drop-in path on CVRP-100 (SURVEY.md 8d config 3 data): ConstructivePolicy +
     CVRPEnv, greedy on a stub decoder (a fixed HBM-resident [B, N+1] logits tensor whose
-    masked argmax is the decoded action), per step one co_decode_step + one co_cvrp_step
-    launch through the native step glue; the episode length is data dependent (polls
+    masked argmax is the decoded action), per step one co_cvrp_decode_step launch (decode +
+    env step) through the native step glue; the episode length is data dependent (polls
     resume once the env's lower bound N+1 is reached).  Plus the host cost per step at
-    B = 64 and the per-step GPU time of the two kernels (HIP events over the episode)."""
+    B = 64, the per-step GPU time (HIP events over the episode) and the fused kernel alone
+    (decode_fused_kernel_us, a mid-episode state)."""
     from rl4co_slap_amd.envs import CVRPEnv
     from rl4co_slap_amd.rollout.constructive import ConstructivePolicy, LogitsDecoder
     from rl4co_slap_amd.td import TensorDict
@@ -992,7 +997,44 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
             out["host_us_per_step_b64"] = t / kk / T * 1e6
         env.decode_and_step, env.native_decode_and_step = real
     out["host_below_kernels"] = out["host_us_per_step_b64"] < out["gpu_us_per_step"]
+    out["decode_fused_kernel_us"] = cvrp_decode_step_kernel_us(b, n, dev)
     return out
+
+
+def cvrp_decode_step_kernel_us(b, n, dev, reps=50):
+    """GPU time of one co_cvrp_decode_step launch (certified greedy, clip 10) on a CVRP-n
+    state five steps into an episode (config 3 data), HIP events on the launch stream."""
+    from rl4co_slap_amd import _native
+    from rl4co_slap_amd.envs import CVRPEnv
+    from rl4co_slap_amd.td import TensorDict
+
+    torch.manual_seed(1)
+    la = torch.rand(b, n + 1, 2)
+    dm = ((torch.rand(b, n) * 9).int() + 1).float() / 50.0
+    env = CVRPEnv(generator_params=dict(num_loc=n), device=dev)
+    td = env.reset(TensorDict({"depot": la[:, 0].to(dev), "locs": la[:, 1:].contiguous().to(dev),
+                               "demand": dm.to(dev)}, batch_size=[b]))
+    for t in range(5):
+        td.set("action", torch.full((b,), 1 + t, dtype=torch.int64, device=dev))
+        td = env.step(td)["next"]
+    logits = torch.randn(b, n + 1, device=dev)
+    act = torch.empty(b, dtype=torch.int64, device=dev)
+    lp = torch.empty(b, device=dev)
+    used = torch.empty_like(td["used_capacity"])
+    vis = torch.empty_like(td["visited"])
+    cur = torch.empty((b, 1), dtype=torch.int64, device=dev)
+    done, rew = (torch.empty(b, dtype=torch.bool, device=dev) for _ in range(2))
+    mask = torch.empty_like(td["action_mask"])
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    p = _native.ptr
+    launch = _native.bind("co_cvrp_decode_step", b, n, p(logits), n + 1, p(td["action_mask"]),
+                          10.0, 1.0, _native.DECODE_CERTIFIED, None, p(act), p(lp), 0, 0,
+                          p(td["demand"]), p(td["used_capacity"]), p(used),
+                          p(td["vehicle_capacity"]), p(td["visited"]), p(vis), p(cur), p(done),
+                          p(rew), p(mask), None, p(st))
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    _, ev = timed(lambda: launch(sh), reps, 5, 1, dev)
+    return ev / reps * 1e6
 
 
 def count_fused_calls(env, calls):

@@ -27,7 +27,13 @@ constexpr bool kDiagCertCount = true;  // logp -23456, rows of tier 2 -12345
 constexpr bool kDiagCertCount = false;
 #endif
 
+#ifdef CO_DIAG_CVRP_CUT  // timing: co_cvrp_decode_step without its transition (1) or decode (2)
+constexpr int kDiagCvrpCut = CO_DIAG_CVRP_CUT;
+#else
+constexpr int kDiagCvrpCut = 0;
+#endif
+
 // a build whose "exact" decode is not exact
-constexpr bool kDiagTimingCut = kDiagFastTanh || kDiagFastExp;
+constexpr bool kDiagTimingCut = kDiagFastTanh || kDiagFastExp || kDiagCvrpCut != 0;
 
 }  // namespace co

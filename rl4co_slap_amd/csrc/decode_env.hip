@@ -308,7 +308,6 @@ struct CvrpStage {
                                         int c0, int64_t a_raw, int32_t* status) const {
     const int Nn = N, NC = N + 1;
     const float* dm_s = reinterpret_cast<const float*>(dem()) + g * Nn;
-    const uint8_t* vb_s = reinterpret_cast<const uint8_t*>(vis()) + g * NC;
     const float used = __uint_as_float(sc()[g]), cap = __uint_as_float(sc()[RPW + g]);
     const bool bad = a_raw < 0 || a_raw > Nn;
     // the selected demand demand[clamp(a - 1, 0, N - 1)]
@@ -324,13 +323,16 @@ struct CvrpStage {
       const int nown = valid ? (NC - c < 0 ? 0 : (NC - c > 4 ? 4 : NC - c)) : 0;
       const uint32_t own = nown >= 4 ? 0xffffffffu : (1u << (8 * nown)) - 1u;
       const uint32_t cust = c == 0 ? own & ~0xffu : own;  // the depot column excluded
-      uint32_t x = 0u;
+      // the chunk's visited bytes: the two stage dwords it straddles, byte-aligned by one
+      // v_alignbyte (reads past the row stay inside the stage / LDS; `own` masks them)
+      const int o = g * NC + c;
+      const uint32_t* v32 = vis() + (o >> 2);
+      uint32_t x = __builtin_amdgcn_alignbyte(v32[1], v32[0], (uint32_t)(o & 3)) & own;
       float d[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool in = q < nown;
-        x |= in ? (uint32_t)vb_s[c + q] << (8 * q) : 0u;
-        d[q] = (in && c + q >= 1) ? dm_s[c + q - 1] : 0.f;
+      for (int q = 0; q < 4; ++q) {  // unconditional reads (index -1 / past the row: LDS
+        const float dr = dm_s[c + q - 1];  // words of the stage or the static area), selected
+        d[q] = (q < nown && c + q >= 1) ? dr : 0.f;
       }
       const int ea = a - c;  // the action's byte, if in this chunk: scatter(..., 1)
       if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
@@ -403,12 +405,16 @@ __global__ __launch_bounds__(256) void cvrp_decode_greedy_kernel(
     const float* lrow = logits + r * lstride;
     const uint8_t* mrow = mask_in + r * (int64_t)NC;
     g.load(valid, NC, lrow, mrow, c0);
-    float lp, lse;
-    const int sel = greedy_row<OPT>(g, valid, NC, clip, temp, sl, c0,
-                                    group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
+    float lp = 0.f, lse = 0.f;
+    int sel = (int)(row % NC);
+    if (kDiagCvrpCut != 2)
+      sel = greedy_row<OPT>(g, valid, NC, clip, temp, sl, c0, group_scratch<RL, EPL>(lds, grp),
+                            lse, lp, lrow, mrow);
+    else
+      lp = g.v[0];  // keep the loads
     const bool feas0 = g.allowed(0);
     stage_ready();
-    st.apply(e, valid, r, grp, sl, c0, sel, status);
+    if (kDiagCvrpCut != 1) st.apply(e, valid, r, grp, sl, c0, sel, status);
     if (valid && sl == 0) {
       if (lse != lse && !feas0) set_status(status, CO_ST_INFEASIBLE);
       action_out[r] = sel;
