@@ -49,17 +49,18 @@ __global__ __launch_bounds__(256) void cvrp_pad_kernel(int64_t B, const int32_t*
 }
 
 // ---------------------------------------------------------------------------------------
-// LDS-row episodes (the default engines).  The per-step cost of the register engines above
-// is the per-candidate VALU work: two subtractions, two products, a sum, the visited /
-// capacity bit test and four selects per node.  Here each lane keeps its slots' y (and CVRP
-// demand) in registers as pairs, and the instance's x row lives in LDS, slot pairs
-// (x_k, x_k+1) of its G lanes adjacent; a visited node (and every padding slot, and the CVRP
-// depot) has x = NaN, so its distance is NaN and it can never be the minimum -- visiting is
-// one LDS store instead of a per-candidate test.  Per pair of candidates: one 8-byte LDS
-// read, five packed f32 operations (v_pk_add / v_pk_mul: the same IEEE operations, two
-// slots at a time), and per candidate a key = the squared distance's bits with the low KB
-// bits replaced by the slot (one v_and_or) folded into the lane's two smallest keys
-// (v_med3_u32 + v_min_u32, two independent chains).  The group merges (min, second min)
+// LDS-row episodes.  The per-step cost of a register-resident engine (round 4: coordinates
+// and a visited bit mask in VGPRs) is the per-candidate VALU work: two subtractions, two
+// products, a sum, the visited / capacity bit test and four selects per node.  Here each
+// lane keeps its slots' y (and CVRP demand) in registers as pairs, and the instance's x row
+// lives in LDS in node order; a visited node (and every padding slot, and the CVRP depot)
+// has x = NaN, so its distance is NaN and it can never be the minimum -- visiting is one
+// LDS store instead of a per-candidate test.  Per pair of candidates: one ds_read2_b32,
+// five packed f32 operations (v_pk_add / v_pk_mul: the same IEEE operations, two slots at
+// a time), and per candidate a key = the squared distance's bits with the low BB bits
+// replaced by slot * G (one v_and_or; the lane's index is ORed in once) folded into the
+// lane's two smallest keys (v_med3_u32 + v_min_u32, two independent chains).  The group
+// merges (min, second min)
 // pairs over DPP, and the winner is exact without a sqrt per candidate:
 //   keys compare as (truncated squared distance, node); with T = the squared distance's
 //   bits with the low BB bits cleared (a relative error below 2^(BB-23)), if the second
@@ -92,33 +93,26 @@ __device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
-// float index of node c's x in its instance's x row: node c is slot c / G of lane c % G,
-// slots in pairs of 8 bytes, a pair's G lanes adjacent
-template <int G>
-__device__ __forceinline__ int lds_xoff(int c) {
-  const unsigned k = (unsigned)c / G, sl = (unsigned)c % G;
-  return (int)(((k >> 1) * G + sl) * 2 + (k & 1));
-}
-
-// the lane's x slot pairs from its instance's LDS row
+// The instance's x row is in node order (node c = slot c / G of lane c % G): a visit and the
+// winner's read address node c directly, and a lane's slot pair (2p, 2p+1) is one
+// ds_read2_b32 (dword offsets 2pG and (2p+1)G from the lane's base) into a register pair.
 template <int G, int EPL>
 __device__ __forceinline__ void lds_load_x(const float* __restrict__ rowx, int sl,
                                            v2f (&x2)[EPL / 2]) {
-  const float2* r2 = reinterpret_cast<const float2*>(rowx);
+  const float* r = rowx + sl;
 #pragma unroll
-  for (int p = 0; p < EPL / 2; ++p) {
-    const float2 q = r2[p * G + sl];
-    x2[p] = (v2f){q.x, q.y};
-  }
+  for (int p = 0; p < EPL / 2; ++p) x2[p] = (v2f){r[2 * p * G], r[(2 * p + 1) * G]};
 }
 
-// the lane's two smallest keys (m1 <= m2) over its EPL slots; DEM: a customer whose demand
-// does not fit (dm + used > vcap, cvrp/env.py:140) gets the key ~0
+// the lane's two smallest keys (m1 <= m2) over its EPL slots, key = the squared distance's
+// bits with the low BB bits replaced by slot * G (the node index less the lane, which the
+// caller ORs in); DEM: a customer whose demand does not fit (dm + used > vcap,
+// cvrp/env.py:140) gets the key ~0
 template <int G, int EPL, bool DEM>
 __device__ __forceinline__ void lds_scan(const v2f (&x2)[EPL / 2], float cx, float cy,
                                          const v2f (&y2)[EPL / 2], const v2f (&dm2)[EPL / 2],
                                          float used, float vcap, uint32_t& m1, uint32_t& m2) {
-  constexpr uint32_t KM = (1u << clog2(EPL)) - 1u;
+  constexpr uint32_t BM = (1u << clog2(G * EPL)) - 1u;
   const v2f cx2 = {cx, cx}, cy2 = {cy, cy};
   const v2f u2 = {used, used};
   uint32_t a1 = 0xffffffffu, a2 = 0xffffffffu, b1 = 0xffffffffu, b2 = 0xffffffffu;
@@ -130,7 +124,7 @@ __device__ __forceinline__ void lds_scan(const v2f (&x2)[EPL / 2], float cx, flo
     if (DEM) du = dm2[p] + u2;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      uint32_t key = (__float_as_uint(s[h]) & ~KM) | (uint32_t)(2 * p + h);
+      uint32_t key = (__float_as_uint(s[h]) & ~BM) | (uint32_t)((2 * p + h) * G);
       if (DEM && du[h] > vcap) key = 0xffffffffu;
       if (p & 1) {  // two independent (min, second min) chains
         b2 = med3u(b1, b2, key);
@@ -190,7 +184,7 @@ __device__ __noinline__ int lds_exact(const float* __restrict__ rowx,
     const int c = k * G + sl;
     const int ci = c < lo ? 0 : (c > hi ? hi - lo : c - lo);  // in range; x is NaN outside
     // NaN for visited / padding / the CVRP depot: never taken
-    const float d = edge_len(cx, cy, rowx[lds_xoff<G>(c)], lrow[ci].y);
+    const float d = edge_len(cx, cy, rowx[c], lrow[ci].y);
     const bool fits = !DEM || !(drow[ci] + used > vcap);
     if (fits && d < best) {
       best = d;
@@ -210,18 +204,19 @@ __device__ __forceinline__ int lds_nearest(const float* __restrict__ rowx,
                                            float used, float vcap,
                                            const float2* __restrict__ lrow,
                                            const float* __restrict__ drow, int lo, int hi) {
-  constexpr uint32_t KM = (1u << clog2(EPL)) - 1u, BM = (1u << clog2(G * EPL)) - 1u;
+  constexpr uint32_t BM = (1u << clog2(G * EPL)) - 1u;
   constexpr float kWin = 1.0f + (float)(1u << clog2(G * EPL)) * 0x1p-20f;
   uint32_t m1, m2;
   lds_scan<G, EPL, DEM>(x2, cx, cy, y2, dm2, used, vcap, m1, m2);
-  // lane keys (T | slot) -> group keys (T | node); slot * G + lane < 2^BB never reaches T
-  m1 = (m1 & ~BM) | ((m1 & KM) * G + sl);
-  m2 = (m2 & ~BM) | ((m2 & KM) * G + sl);
+  m1 |= (uint32_t)sl;  // lane keys (T | slot * G) -> group keys (T | node)
+  m2 |= (uint32_t)sl;
   grp_min2<G>(m1, m2);
   const uint32_t t1 = m1 & ~BM, t2 = m2 & ~BM;
-  const bool none = t1 >= 0x7fc00000u;  // every slot NaN or ~0
-  const bool ok = none || (t1 >= 0x0d800000u && t1 < 0x7f800000u &&
-                           t2 > __float_as_uint(__uint_as_float(t1) * kWin));
+  // one bitwise test (no short-circuit branches): every slot poisoned (NaN or ~0), or a
+  // normal finite winner whose next key is outside the ratio window
+  const bool none = t1 >= 0x7fc00000u;
+  const bool ok = none | ((t1 - 0x0d800000u < 0x7f800000u - 0x0d800000u) &
+                          (t2 > __float_as_uint(__uint_as_float(t1) * kWin)));
   int w = none ? kNoNode : (int)(m1 & BM);
   if (__builtin_expect(__any(!ok), 0))
     w = lds_exact<G, EPL, DEM>(rowx, lrow, drow, lo, hi, sl, cx, cy, used, vcap);
@@ -240,7 +235,8 @@ struct TermAcc {
   __device__ __forceinline__ void add(float sq, int t, int sl) {
     const int r = t & (G - 1);  // wave-uniform
     hold = sl == r ? sq : hold;
-    if (r == G - 1) {
+    if (r == G - 1) {  // a real branch: the compiler would if-convert it (a sqrt every step)
+      asm volatile("");
       sum += (double)__builtin_sqrtf(hold);
       hold = 0.f;
     }
@@ -274,7 +270,7 @@ __global__ __launch_bounds__(64) void tsp_nearest_lds_kernel(
   for (int k = 0; k < EPL; ++k) {  // padding slots: x NaN (loads unconditional: no serial waits)
     const int c = k * G + sl;
     const float2 q = lrow[c < N ? c : N - 1];
-    rowx[lds_xoff<G>(c)] = c < N ? q.x : qnan;
+    rowx[c] = c < N ? q.x : qnan;
     y2[k >> 1][k & 1] = c < N ? q.y : 0.f;
   }
   const v2f nodem[EPL / 2] = {};  // no demand
@@ -291,7 +287,7 @@ __global__ __launch_bounds__(64) void tsp_nearest_lds_kernel(
     int a = lds_nearest<G, EPL, false>(rowx, x2, sl, cx, cy, y2, nodem, 0.f, 0.f, lrow,
                                        nullptr, 0, N - 1);
     a = a == kNoNode ? 0 : a;  // only when every remaining distance is infinite
-    float* px = rowx + lds_xoff<G>(a);
+    float* px = rowx + a;
     const float2 wq = lrow[a];  // an L2 read: the winner's y is in its owner lane's VGPRs
     const float wx = wq.x, wy = wq.y;
     *px = qnan;  // visited
@@ -361,7 +357,7 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
     const float2 q = c == 0 ? dep : (c <= N ? lq : make_float2(qnan, 0.f));
     const float d = (c >= 1 && c <= N) ? ld : 0.f;
     if (valid && locs_out && c <= N) locs_out[bb * M + c] = q;
-    rowx[lds_xoff<G>(c)] = c == 0 ? qnan : q.x;  // the depot is never a nearest candidate
+    rowx[c] = c == 0 ? qnan : q.x;  // the depot is never a nearest candidate
     y2[k >> 1][k & 1] = q.y;
     dm2[k >> 1][k & 1] = d;
   }
@@ -380,7 +376,7 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
     const int w = lds_nearest<G, EPL, true>(rowx, x2, sl, cx, cy, y2, dm2, used, vcap, lrow,
                                             drow, 1, N);
     const int a = w == kNoNode ? 0 : w;
-    float* px = rowx + lds_xoff<G>(a);
+    float* px = rowx + a;
     const int ai = a == 0 ? 0 : a - 1;
     const float2 wq = lrow[ai];  // L2 reads
     const float wx = wq.x, wy = wq.y, wd = drow[ai];
@@ -410,7 +406,7 @@ __global__ __launch_bounds__(64) void cvrp_nearest_lds_kernel(
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
     const int c = k * G + sl;
-    const bool v = c == 0 ? (st >> 31) != 0 : __builtin_isnan(rowx[lds_xoff<G>(c)]);
+    const bool v = c == 0 ? (st >> 31) != 0 : __builtin_isnan(rowx[c]);
     const bool feas = c >= 1 && c <= N && !v && !(dm2[k >> 1][k & 1] + used > vcap);
     any_feas |= feas;
     if (valid && c <= N) {
