@@ -61,6 +61,20 @@ for blocks, threads in ((2048, 256), (8192, 64), (4096, 128), (1024, 512), (512,
         lambda: lc.ceiling_touch(blocks, threads, 1, src.data_ptr(), dst.data_ptr(), sh))
 res["empty_256x256"] = ev_us(lambda: lc.ceiling_empty(256, 256, 1, sink.data_ptr(), sh))
 res["empty_1x64"] = ev_us(lambda: lc.ceiling_empty(1, 64, 1, sink.data_ptr(), sh))
+# the same launches issued from C in one call (no Python / ctypes per launch) and replayed
+# from a HIP graph: what the GPU side costs per kernel boundary once the host is not the
+# bottleneck
+for blocks, threads in ((1, 64), (2048, 256)):
+    res[f"empty_{blocks}x{threads}_c_loop"] = round(ev_us(
+        lambda: lc.ceiling_empty(blocks, threads, 50, sink.data_ptr(), sh), reps=4) / 50, 3)
+    gs = torch.cuda.Stream(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(gs):
+        lc.ceiling_empty(blocks, threads, 1, sink.data_ptr(), gs.cuda_stream)  # warm
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=gs):
+            lc.ceiling_empty(blocks, threads, 50, sink.data_ptr(), gs.cuda_stream)
+    res[f"empty_{blocks}x{threads}_graph"] = round(ev_us(lambda: g.replay(), reps=4) / 50, 3)
 
 
 def copy_us(nbytes):
