@@ -198,13 +198,39 @@ def time_bound(f, dev, reps=50):
     return e0.elapsed_time(e1) / 1e3 / reps
 
 
+def time_graph(f, dev, reps=50):
+    """Average HIP-event time (s) per launch of `reps` launches of a bound C-ABI call replayed
+    from one HIP graph: the GPU-side time per kernel, without the host's issue rate
+    (eager launches from Python cost >= 3.6 us each even for an empty kernel:
+    tools/launch_ceiling.py)."""
+    gs = torch.cuda.Stream(dev)
+    with torch.cuda.stream(gs):
+        f(gs.cuda_stream)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=gs):
+            for _ in range(reps):
+                f(gs.cuda_stream)
+    g.replay()
+    torch.cuda.synchronize(dev)
+    rs = torch.cuda.current_stream(dev)  # replay() runs on the current stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(rs)
+    g.replay()
+    e1.record(rs)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / 1e3 / reps
+
+
 def step_kernels_vs_copy(dev):
     """Each stepwise env kernel alone (one launch = one env step over the batch, state
     re-read from where the previous launch left it, as in the stepwise graphs) beside
     co_probe_copy moving the same bytes through the same kind of buffer (one buffer pair
     reused, i.e. Infinity-Cache resident like the stepwise state): the small-launch
     ceiling a step kernel of that size can reach.  Bytes per env
-    step: SURVEY.md 8d (TSP 2N+50, CVRP 7N+33, SLAP 2L+34)."""
+    step: SURVEY.md 8d (TSP 2N+50, CVRP 7N+33, SLAP 2L+34).  Both timed as HIP-graph
+    replays (time_graph: the GPU-side time per launch, as inside the stepwise graphs); the
+    eager (Python-issued) times beside them sit at the host's issue floor for the copy."""
     from rl4co_slap_amd import _native as nat
 
     out = {}
@@ -213,13 +239,16 @@ def step_kernels_vs_copy(dev):
     def copy_us(nbytes):
         n = (nbytes // 2) // 16 * 16
         a, c = torch.ones(n, dtype=torch.uint8, device=d), torch.empty(n, dtype=torch.uint8, device=d)
-        return time_bound(nat.bind("co_probe_copy", nat.ptr(a), nat.ptr(c), n), d) * 1e6
+        f = nat.bind("co_probe_copy", nat.ptr(a), nat.ptr(c), n)
+        return time_graph(f, d) * 1e6, time_bound(f, d) * 1e6
 
-    def rec(name, us, nbytes):
-        cu = copy_us(nbytes)
+    def rec(name, f, nbytes):
+        us, us_eager = time_graph(f, d) * 1e6, time_bound(f, d) * 1e6
+        cu, cu_eager = copy_us(nbytes)
         out[name] = {"bytes": nbytes, "kernel_us": us, "kernel_GBps": nbytes / us / 1e3,
                      "copy_same_bytes_us": cu, "copy_GBps": nbytes / cu / 1e3,
-                     "frac_of_copy": cu / us, "hbm_frac": nbytes / us / 1e3 / HBM_PEAK_GBS}
+                     "frac_of_copy": cu / us, "hbm_frac": nbytes / us / 1e3 / HBM_PEAK_GBS,
+                     "kernel_us_eager": us_eager, "copy_same_bytes_us_eager": cu_eager}
 
     # TSP-100, B = 65,536 (co_tsp_step, first_mode 0)
     b, n = 65536, 100
@@ -232,7 +261,7 @@ def step_kernels_vs_copy(dev):
     f = nat.bind("co_tsp_step", b, n, nat.ptr(act), nat.ptr(mask), nat.ptr(mask), nat.ptr(i),
                  nat.ptr(i), nat.ptr(first), nat.ptr(first), nat.ptr(cur), nat.ptr(done),
                  nat.ptr(rw), 0, None, nat.ptr(st))
-    rec("tsp_step_b65536", time_bound(f, d) * 1e6, b * (2 * n + 50))
+    rec("tsp_step_b65536", f, b * (2 * n + 50))
     del act, mask, i, first, cur, done, rw
     # CVRP-100, B = 32,768 (co_cvrp_step, fused mask)
     b = 32768
@@ -247,7 +276,7 @@ def step_kernels_vs_copy(dev):
     f = nat.bind("co_cvrp_step", b, n, nat.ptr(act), nat.ptr(dem), nat.ptr(used), nat.ptr(used2),
                  nat.ptr(vcap), nat.ptr(vis), nat.ptr(vis), nat.ptr(cur), nat.ptr(done), nat.ptr(rw),
                  nat.ptr(m), nat.ptr(st), None)
-    rec("cvrp_step_b32768", time_bound(f, d) * 1e6, b * (7 * n + 33))
+    rec("cvrp_step_b32768", f, b * (7 * n + 33))
     del act, dem, used, used2, vcap, vis, cur, done, rw, m
     # SLAP, B = 16,384, L = 100, P = 20 (co_slap_step, in-place assignment)
     b, l, pp = 16384, 100, 20
@@ -260,13 +289,13 @@ def step_kernels_vs_copy(dev):
     f = nat.bind("co_slap_step", b, l, pp, nat.ptr(act), nat.ptr(tc), pp, nat.ptr(asg), nat.ptr(asg),
                  nat.ptr(mask), nat.ptr(mask), nat.ptr(i), nat.ptr(i), nat.ptr(done), nat.ptr(rw),
                  nat.ptr(st))
-    rec("slap_step_b16384", time_bound(f, d) * 1e6, b * (2 * l + 34))
+    rec("slap_step_b16384", f, b * (2 * l + 34))
     # the bench policy fused with it (co_slap_closest_step): + depot distances 4L read
     dd = torch.rand(b, l, device=d)
     f = nat.bind("co_slap_closest_step", b, l, pp, nat.ptr(dd), nat.ptr(tc), pp, nat.ptr(asg),
                  nat.ptr(asg), nat.ptr(mask), nat.ptr(mask), nat.ptr(act), nat.ptr(i), nat.ptr(i), nat.ptr(done),
                  nat.ptr(rw), nat.ptr(st))
-    rec("slap_closest_step_b16384", time_bound(f, d) * 1e6, b * (6 * l + 34))
+    rec("slap_closest_step_b16384", f, b * (6 * l + 34))
     return out
 
 
