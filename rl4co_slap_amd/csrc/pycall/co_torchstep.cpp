@@ -167,7 +167,14 @@ struct Slab {
   int64_t off = 0, cap = 0, fresh_steps = 0;
   // a region of nbytes (a multiple of kAlign): offset into `st`
   int64_t take(const c10::Device& d, int64_t nbytes) {
-    if (!st || d != dev || off + nbytes > cap || fresh_steps > 0) {
+    if (fresh_steps > 0 && st && d == dev && st.use_count() == 1 &&
+        nbytes * fresh_steps <= (int64_t)st.nbytes()) {
+      // an episode start on a slab nothing refers to any more (the last episode's row
+      // views are gone): rewrite it from the top, in stream order, instead of allocating
+      cap = (int64_t)st.nbytes();
+      fresh_steps = 0;
+      off = 0;
+    } else if (!st || d != dev || off + nbytes > cap || fresh_steps > 0) {
       cap = nbytes * (fresh_steps > 0 ? fresh_steps : kSteps);
       fresh_steps = 0;
       st = new_storage(d, cap);
@@ -934,12 +941,15 @@ PyObject* episode_stack(PyObject*, PyObject* const* a, Py_ssize_t n) {
       if (T == 1) rs[li] = b;
     }
     if (status.device() != dev || status.scalar_type() != at::kInt) Py_RETURN_NONE;
-    const auto o64 = at::TensorOptions().device(dev).dtype(at::kLong);
-    const auto o32 = at::TensorOptions().device(dev).dtype(at::kFloat);
-    at::Tensor acts = at::empty({b, (int64_t)T}, o64);
-    at::Tensor lps = at::empty({b, (int64_t)T}, o32);
+    // the three outputs carved from one storage (one allocation instead of three)
+    Carver cv;
+    const int64_t oa = cv.take(8 * b * (int64_t)T), ol = cv.take(4 * b * (int64_t)T),
+                  os = cv.take(4 * b);
+    const c10::Storage ost = new_storage(dev, cv.off);
+    at::Tensor acts = view_of(ost, at::kLong, oa, {b, (int64_t)T});
+    at::Tensor lps = view_of(ost, at::kFloat, ol, {b, (int64_t)T});
     at::Tensor ll;
-    if (want_ll) ll = at::empty({b}, o32);
+    if (want_ll) ll = view_of(ost, at::kFloat, os, {b});
     void* stream = current_stream(dev);
     int rc;
     Py_BEGIN_ALLOW_THREADS
