@@ -169,3 +169,32 @@ def test_glue_epilogue_routing_tsp_cvrp(dev, env_cls):
     ref = lps.double().sum(1).float()
     assert ((ll - ref).abs() <= ref.abs() * 2.0 ** -23).all()
     assert acts.shape == (b, steps)
+
+
+def test_slab_reused_only_when_unreferenced(dev):
+    """An episode start rewrites the step glue's slab only when no view of it is left: the
+    caller's td from the first episode still holds its last `action` (a slab row), so the
+    second episode must take a new slab and leave that row intact; once dropped, a third
+    episode may reuse it -- actions always equal the first-episode values."""
+    b = 48
+    data = _slap_data(b, dev, 11)
+    logits = torch.randn(b, 100, generator=torch.Generator().manual_seed(6)).to(dev)
+    env = SLAPEnv(device=dev)
+    pol = ConstructivePolicy(None, LogitsDecoder(lambda t: logits), env_name="slap")
+    td1 = env.reset(TensorDict(dict(data.items()), [b]))
+    out1 = pol(td1, env, phase="test", decode_type="greedy", return_actions=True)
+    kept = td1["action"]
+    snap = kept.clone()
+    assert torch.equal(snap, out1["actions"][:, -1])
+    for _ in range(2):
+        td2 = env.reset(TensorDict(dict(data.items()), [b]))
+        out2 = pol(td2, env, phase="test", decode_type="greedy", return_actions=True)
+        torch.cuda.synchronize()
+        assert torch.equal(kept, snap)
+        assert torch.equal(out2["actions"], out1["actions"])
+        assert torch.equal(out2["log_likelihood"], out1["log_likelihood"])
+        del td2, out2
+    del kept, td1
+    td3 = env.reset(TensorDict(dict(data.items()), [b]))
+    out3 = pol(td3, env, phase="test", decode_type="greedy", return_actions=True)
+    assert torch.equal(out3["actions"], out1["actions"])
