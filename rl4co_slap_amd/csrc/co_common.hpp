@@ -12,6 +12,12 @@ namespace co {
 constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+// the wave's index in its block as a wave-uniform (SGPR) value.  `threadIdx.x >> 6` alone is
+// a VGPR to the compiler, and everything derived from it (row bases, LDS-DMA counts, m0 and
+// global addresses) becomes per-lane VALU work and exec-masked loops.
+__device__ __forceinline__ int wave_in_block() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
@@ -240,7 +246,7 @@ typedef __attribute__((address_space(3))) void lds_void;
 // vmcnt drain + workgroup barrier that make the tile visible.
 __device__ __forceinline__ void stage_bytes_lds(const unsigned char* __restrict__ src, int nbytes,
                                                 unsigned char* dst) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_in_block(), nw = blockDim.x >> 6;
   const int n16 = nbytes & ~15;
   for (int base = wave * 1024; base < n16; base += nw * 1024) {
     const int off = base + lane * 16;

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void cvrp_reset_kernel(int64_t B, int N, const
                                                          uint8_t* visited, uint8_t* mask) {
   const int lane = lane_id();
   const int64_t wpb = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_in_block(); b < B;
        b += (int64_t)gridDim.x * wpb) {
     float2* lo = locs_out + b * (N + 1);
     const float2* li = locs_in + b * (int64_t)N;
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void cvrp_step_kernel(
   const int lane = lane_id();
   const int64_t wpb = blockDim.x >> 6;
   int left = 0;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_in_block(); b < B;
        b += (int64_t)gridDim.x * wpb) {
     const int64_t a = action[b];
     const bool bad = a < 0 || a > N;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(64 * WAVES) void cvrp_step_rows_kernel(
     uint8_t* __restrict__ mask, int32_t* status, int32_t* not_done) {
   __shared__ int s_left[WAVES];
   constexpr int RW = 64 / G;  // rows per wave
-  const int lane = lane_id(), w = threadIdx.x >> 6, sl = lane % G, grp = lane / G;
+  const int lane = lane_id(), w = wave_in_block(), sl = lane % G, grp = lane / G;
   const int NC = N + 1;
   const int64_t wrow0 = ((int64_t)blockIdx.x * WAVES + w) * (RW * Q);
   int left = 0;
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void cvrp_nearest_group_kernel(int64_t B, int 
                                                                  int64_t* __restrict__ out) {
   const int lane = lane_id(), sl = lane % G;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const int K = (N + G - 1) / G;
   for (int64_t base = wid * (64 / G); base < B; base += nwaves * (64 / G)) {
     const int64_t b = base + lane / G;
@@ -754,7 +754,7 @@ __global__ __launch_bounds__(256) void cvrp_mask_kernel(int64_t B, int N, const 
                                                         const uint8_t* visited,
                                                         const int64_t* cur, uint8_t* mask) {
   const int64_t wpb = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_in_block(); b < B;
        b += (int64_t)gridDim.x * wpb) {
     cvrp_row(N, demand + b * (int64_t)N, used[b], vcap[b], visited + b * (N + 1), nullptr, -1,
              cur[b], mask + b * (N + 1));
@@ -767,7 +767,7 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
     int64_t B, int N, int T, const float2* locs, const int64_t* actions, int64_t sb, int64_t st,
     const float* demand, const float* vcap, int check, float* reward, int32_t* status) {
   extern __shared__ uint32_t s_mem[];
-  const int w = threadIdx.x >> 6, lane = lane_id();
+  const int w = wave_in_block(), lane = lane_id();
   const int words = (N + 32) >> 5;  // bits for values 0..N
   uint32_t* bits = s_mem + w * (words + 4 * T);
   float* dseq = reinterpret_cast<float*>(bits + words);
@@ -965,7 +965,7 @@ __global__ __launch_bounds__(64 * Q) void cvrp_reward_tile_kernel(
   double* s_len = reinterpret_cast<double*>(smem + L.len);
   __shared__ float2 s_last[64];  // the point after step T-1 (closing edge)
   __shared__ int s_lok[64], s_range[64], s_cnt[64], s_over[64];
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, q = wave_in_block();
   const int64_t row0 = (int64_t)blockIdx.x * 64;
   const int rows = (int)((B - row0) < 64 ? (B - row0) : 64);
   const bool live = lane < rows;

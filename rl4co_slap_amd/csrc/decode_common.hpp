@@ -99,7 +99,7 @@ __device__ __forceinline__ float row_log_sum_exp(const float (&d)[EPL], int N, i
 // (unused, and dropped by the compiler, on the fast path)
 template <int RL, int EPL>
 __device__ __forceinline__ float* group_scratch(float* lds, int grp) {
-  return lds + (threadIdx.x >> 6) * (64 * EPL) + grp * (RL * EPL);
+  return lds + wave_in_block() * (64 * EPL) + grp * (RL * EPL);
 }
 
 // Exact tanh (tanh_cr) of the elements a lane marks `ok`, wave-compacted: a masked
@@ -713,7 +713,7 @@ __global__ __launch_bounds__(256) void decode_greedy_kernel(
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   // one row group per wave: the grid covers B (no grid-stride loop, so no values are
   // hoisted into registers across row groups -- r04: certified 71 -> fewer VGPRs)
   const int64_t base = wid * RPW;
@@ -752,7 +752,7 @@ __global__ __launch_bounds__(256) void decode_kernel(int64_t B, int N, const flo
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   // one row group per wave: the grid covers B (no grid-stride loop, so no values are
   // hoisted into registers across row groups -- r04: certified 71 -> fewer VGPRs)
   const int64_t base = wid * RPW;
@@ -798,7 +798,7 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL;
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
   // UNR rows per lane group per iteration: every load of all UNR rows (logits, mask,
   // i, first_node, action, ll accumulator) is issued before any row's math
@@ -880,7 +880,7 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
   // one row group per wave: the grid covers B (no grid-stride loop, so no values are
   // hoisted into registers across row groups -- r04: certified 71 -> fewer VGPRs)

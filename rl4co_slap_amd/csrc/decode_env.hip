@@ -140,10 +140,10 @@ __global__ __launch_bounds__(256) void slap_decode_greedy_kernel(
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const SlapStage<RL> st{s_stage + (threadIdx.x >> 6) * slap_stage_dwords(RPW, e.P), e.P};
+  const SlapStage<RL> st{s_stage + wave_in_block() * slap_stage_dwords(RPW, e.P), e.P};
   // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
   // registers across row groups)
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const int64_t base = wid * RPW;
   if (base >= B) return;  // wave-uniform
   {
@@ -191,10 +191,10 @@ __global__ __launch_bounds__(256) void slap_decode_step_kernel(
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const SlapStage<RL> st{s_stage + (threadIdx.x >> 6) * slap_stage_dwords(RPW, e.P), e.P};
+  const SlapStage<RL> st{s_stage + wave_in_block() * slap_stage_dwords(RPW, e.P), e.P};
   // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
   // registers across row groups)
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const int64_t base = wid * RPW;
   if (base >= B) return;  // wave-uniform
   {
@@ -389,10 +389,10 @@ __global__ __launch_bounds__(256) void cvrp_decode_greedy_kernel(
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const CvrpStage<RL, EPL> st{s_stage + (threadIdx.x >> 6) * cvrp_stage_dwords(RPW, e.N), e.N};
+  const CvrpStage<RL, EPL> st{s_stage + wave_in_block() * cvrp_stage_dwords(RPW, e.N), e.N};
   // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
   // registers across row groups)
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const int64_t base = wid * RPW;
   if (base >= B) return;  // wave-uniform
   {
@@ -434,10 +434,10 @@ __global__ __launch_bounds__(256) void cvrp_decode_step_kernel(
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const CvrpStage<RL, EPL> st{s_stage + (threadIdx.x >> 6) * cvrp_stage_dwords(RPW, e.N), e.N};
+  const CvrpStage<RL, EPL> st{s_stage + wave_in_block() * cvrp_stage_dwords(RPW, e.N), e.N};
   // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
   // registers across row groups)
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const int64_t base = wid * RPW;
   if (base >= B) return;  // wave-uniform
   {

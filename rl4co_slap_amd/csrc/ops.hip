@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void pomo_baseline_kernel(int64_t B, int S, co
                                                             float* adv, float* lterm) {
   const int lane = lane_id();
   const int64_t wpb = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_in_block(); b < B;
        b += (int64_t)gridDim.x * wpb) {
     float sum = 0.f, mv = -__builtin_inff();
     int mi = 0x7fffffff;
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(1024) void row_deficit_kernel(const uint8_t* __rest
                                                            int64_t n_rows, int width,
                                                            int64_t stride, int32_t* out) {
   __shared__ int s_best[16];
-  const int lane = lane_id(), sl = lane & 15, w = threadIdx.x >> 6;
+  const int lane = lane_id(), sl = lane & 15, w = wave_in_block();
   int best = 0;
   for (int64_t base = ((int64_t)blockIdx.x * 16 + w) * 4; base < n_rows;
        base += (int64_t)gridDim.x * 64) {  // wave-uniform: the group reduction needs all lanes

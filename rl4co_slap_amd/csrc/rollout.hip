@@ -121,7 +121,7 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
   float2* s_xy = reinterpret_cast<float2*>(smem);  // [64][N] coordinates, later scratch
   constexpr int VS = 2 * NW + 1;                    // visited words per instance (odd)
   uint32_t* s_vis = reinterpret_cast<uint32_t*>(smem + tsp_tile_bytes(N, Q));
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, q = wave_in_block();
   const int64_t row0 = (int64_t)blockIdx.x * 64;
   const int rows = (int)((B - row0) < 64 ? (B - row0) : 64);
   const int64_t b = row0 + lane;
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
   __shared__ uint32_t s_bits[4][GPW][(G * EPL + 31) / 32];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_rows[];  // DMA: per wave
   constexpr int NWB = (G * EPL + 31) / 32;
-  const int lane = lane_id(), sl = lane % G, grp = lane / G, w = threadIdx.x >> 6;
+  const int lane = lane_id(), sl = lane % G, grp = lane / G, w = wave_in_block();
   uint32_t* bits = s_bits[w][grp];
   const size_t half = DMA ? tsp_rows_wave_bytes(GPW, N) / 2 : 0;
   unsigned char* s_w = s_rows + (DMA ? (size_t)w * 2 * half : 0);
@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
   const int lane = lane_id(), sl = lane % G, g = threadIdx.x / G, gw = lane / G;
   int32_t* s_asg = reinterpret_cast<int32_t*>(smem);
   unsigned char* wreg = smem + slap_asg_bytes(IPB, P) +
-                        (size_t)(threadIdx.x >> 6) * slap_wave_bytes(GPW, EPL, L, O, K);
+                        (size_t)wave_in_block() * slap_wave_bytes(GPW, EPL, L, O, K);
   uint64_t* s_keys = reinterpret_cast<uint64_t*>(wreg);
   const int64_t b = (int64_t)blockIdx.x * IPB + g;
   const bool live = b < B;
@@ -861,7 +861,7 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
   // instead of one per step)
   if (CLOSEST) {
     constexpr int IPW = 64 / G;
-    const int w0 = (threadIdx.x >> 6) * IPW;  // first group of this wave
+    const int w0 = wave_in_block() * IPW;  // first group of this wave
     for (int idx = lane; idx < IPW * P; idx += 64) {
       const int t = idx / IPW, gi = idx - t * IPW;
       const int64_t be = (int64_t)blockIdx.x * IPB + w0 + gi;

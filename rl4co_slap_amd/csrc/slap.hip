@@ -120,7 +120,7 @@ __global__ __launch_bounds__(WAVES * 64) void slap_reward_kernel(
   // the picklist -> assignment -> location chain), then the pick points [S] and the
   // per-order lengths [O].
   extern __shared__ float s_rew[];
-  const int w = threadIdx.x >> 6, lane = lane_id();
+  const int w = wave_in_block(), lane = lane_id();
   const int S = O * K;
   float2* lxy = reinterpret_cast<float2*>(s_rew) + (size_t)w * (L + S + O + (P + 1) / 2);
   float2* pts = lxy + L;
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void slap_reward_global_kernel(
     float* __restrict__ reward, int32_t* status) {
   const int lane = lane_id();
   const int64_t wpb = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_in_block(); b < B;
        b += (int64_t)gridDim.x * wpb) {
     const int64_t* prow = picklist + b * (int64_t)O * K;
     const int32_t* arow = assignment + b * (int64_t)P;
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void slap_closest_kernel(int64_t B, int L, con
                                                            const uint8_t* mask, int64_t* out) {
   const int lane = lane_id();
   const int64_t wpb = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_in_block(); b < B;
        b += (int64_t)gridDim.x * wpb) {
     const float* drow = dist + b * (int64_t)L;
     const uint8_t* mrow = mask + b * (int64_t)L;

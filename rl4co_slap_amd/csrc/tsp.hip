@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
   constexpr int WPL = CO_TSP_WPL, U = CO_TSP_UNR;
   const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
   const int W = N >> 2;  // words per row
-  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
   if (first_mode == 2) epi.take_first = (*first_flag != 0);
   // U row groups per wave (the grid covers B; no grid-stride loop)
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(WAVES * 64) void tsp_reward_kernel(int64_t B, int N
                                                                 int64_t sb, int64_t st, int check,
                                                                 float* reward, int32_t* status) {
   extern __shared__ uint32_t s_bits[];
-  const int w = threadIdx.x >> 6, lane = lane_id();
+  const int w = wave_in_block(), lane = lane_id();
   const int words = (T + 31) >> 5;
   uint32_t* bits = s_bits + w * words;
   for (int64_t b = (int64_t)blockIdx.x * WAVES + w; b < B; b += (int64_t)gridDim.x * WAVES) {
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void tsp_nearest_kernel(int64_t B, int N, cons
                                                           int first_step, int64_t* out) {
   const int lane = lane_id();
   const int64_t wpb = blockDim.x >> 6;
-  for (int64_t b = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); b < B;
+  for (int64_t b = (int64_t)blockIdx.x * wpb + wave_in_block(); b < B;
        b += (int64_t)gridDim.x * wpb) {
     if (first_step) {
       if (lane == 0) out[b] = 0;
