@@ -420,6 +420,18 @@ struct Chunk<3> {
   using F = f4_align4;
   using M = u32_align1;
 };
+template <>
+struct Chunk<2> : Chunk<3> {};
+
+// v_cndmask_b32 on a per-lane condition, kept a select: LLVM turned the load's select
+// chains into divergent branches, whose joins then wait for every load in flight
+__device__ __forceinline__ float lane_select(bool c, float t, float f) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3"
+      : "=v"(r)
+      : "v"(f), "v"(t), "s"(__builtin_amdgcn_ballot_w64(c)));
+  return r;
+}
 
 template <int RL, int EPL, int VW>
 struct GreedyRow {
@@ -432,6 +444,10 @@ struct GreedyRow {
                                        int c0) {
     using F = typename Chunk<VW>::F;
     using M = typename Chunk<VW>::M;
+    if constexpr (VW == 3) {
+      load_clamped(valid, N, lrow, mrow, c0);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {
       const int c = c0 + 4 * j;
@@ -444,7 +460,7 @@ struct GreedyRow {
         xf[2] = x[2];
         xf[3] = x[3];
         m = mrow ? (uint32_t) * reinterpret_cast<const M*>(mrow + c) : 0x01010101u;
-      } else if (VW == 3 && valid && c < N) {  // the row's partial last chunk
+      } else if (VW == 2 && valid && c < N) {  // the row's partial last chunk
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           if (c + q < N) {
@@ -457,6 +473,40 @@ struct GreedyRow {
       mw[j] = m;
     }
   }
+  // VW = 3 (rows of any alignment, N >= 4; VW = 2: N < 4, element by element): every chunk
+  // by one 16-byte and one 4-byte access, no branch.  A chunk's start is clamped to the
+  // row's last four columns (cb = min(c, N - 4)): the row's partial last chunk reads columns
+  // N - 4 .. N - 1 and shifts them down by S = 4 - N % 4 (its slots past the row are
+  // masked); a chunk past the row reads the row's tail again and is masked whole.  r05: the
+  // element-wise tail of the branchy form made the compiler wait for each chunk's load
+  // before issuing the next (CVRP-100 rows, N + 1 = 101 columns).
+  __device__ __forceinline__ void load_clamped(bool valid, int N, const float* lrow,
+                                               const uint8_t* mrow, int c0) {
+    using F = typename Chunk<3>::F;
+    using M = typename Chunk<3>::M;
+    const int S = (4 - (N & 3)) & 3;
+    F x[EPL / 4];
+    uint32_t w[EPL / 4];
+#pragma unroll
+    for (int j = 0; j < EPL / 4; ++j) {  // every load issued before the first use
+      const int c = c0 + 4 * j;
+      const int cb = c < N - 4 ? c : N - 4;
+      x[j] = *reinterpret_cast<const F*>(lrow + cb);
+      w[j] = mrow ? (uint32_t) * reinterpret_cast<const M*>(mrow + cb) : 0x01010101u;
+    }
+#pragma unroll
+    for (int j = 0; j < EPL / 4; ++j) {
+      const int c = c0 + 4 * j;
+      const int s = c - (c < N - 4 ? c : N - 4);  // 0: whole chunk, S: partial, >= 4: past
+      const int p = s != 0 ? S : 0;               // the slots' shift
+      v[4 * j + 0] = lane_select(p == 0, x[j][0],
+                                 lane_select(p == 1, x[j][1], lane_select(p == 2, x[j][2], x[j][3])));
+      v[4 * j + 1] = lane_select(p == 0, x[j][1], lane_select(p == 1, x[j][2], x[j][3]));
+      v[4 * j + 2] = lane_select(p == 0, x[j][2], x[j][3]);
+      v[4 * j + 3] = x[j][3];
+      mw[j] = (valid && s < 4) ? w[j] >> ((8 * s) & 31) : 0u;
+    }
+  }
 
   // the row's mask words / logp values back to memory (pad chunks skipped)
   __device__ __forceinline__ void store_mask(int N, uint8_t* orow, int c0) const {
@@ -466,7 +516,7 @@ struct GreedyRow {
       const int c = c0 + 4 * j;
       if (c + 4 <= N) {
         *reinterpret_cast<M*>(orow + c) = (M)mw[j];
-      } else if (VW == 3 && c < N) {
+      } else if (VW != 4 && c < N) {
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           if (c + q < N) orow[c + q] = (uint8_t)(mw[j] >> (8 * q));
@@ -485,7 +535,7 @@ struct GreedyRow {
         x[2] = v[4 * j + 2] - L;
         x[3] = v[4 * j + 3] - L;
         *reinterpret_cast<F*>(frow + c) = x;
-      } else if (VW == 3 && c < N) {
+      } else if (VW != 4 && c < N) {
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           if (c + q < N) frow[c + q] = v[4 * j + q] - L;
@@ -1189,7 +1239,7 @@ inline int greedy_vw(int64_t N, int64_t lstride, const float* logits, const uint
   const uintptr_t f = reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(full);
   const uintptr_t m = reinterpret_cast<uintptr_t>(m_in) | reinterpret_cast<uintptr_t>(m_out);
   if (N % 4 == 0 && lstride % 4 == 0 && (f & 15) == 0 && (m & 3) == 0) return 4;
-  return 3;  // 4-element chunks on rows of any N and alignment
+  return N >= 4 ? 3 : 2;  // 4-element chunks on rows of any N and alignment (2: N < 4)
 }
 
 inline bool decode_vec_ok(const float* logits, int64_t lstride, const uint8_t* mask, int64_t N) {

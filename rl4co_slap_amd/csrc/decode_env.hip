@@ -317,6 +317,22 @@ struct CvrpStage {
     uint32_t vw[EPL / 4], mk[EPL / 4];
     uint32_t cnt = 0u;
     bool feas = false;
+    // every stage read first and unconditionally (index -1 / past the row: LDS words of the
+    // stage or the static area, selected below); the empty volatile asm keeps them
+    // unconditional -- else each demand read is sunk into a per-slot branch
+    float dr[EPL];
+    uint32_t vlo[EPL / 4], vhi[EPL / 4];
+#pragma unroll
+    for (int j = 0; j < EPL / 4; ++j) {
+      const int c = c0 + 4 * j, o = g * NC + c;
+      const uint32_t* v32 = vis() + (o >> 2);
+      vlo[j] = v32[0];
+      vhi[j] = v32[1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dr[4 * j + q] = dm_s[c + q - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) asm volatile("" : "+v"(dr[k]));
 #pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {
       const int c = c0 + 4 * j;
@@ -326,14 +342,10 @@ struct CvrpStage {
       // the chunk's visited bytes: the two stage dwords it straddles, byte-aligned by one
       // v_alignbyte (reads past the row stay inside the stage / LDS; `own` masks them)
       const int o = g * NC + c;
-      const uint32_t* v32 = vis() + (o >> 2);
-      uint32_t x = __builtin_amdgcn_alignbyte(v32[1], v32[0], (uint32_t)(o & 3)) & own;
+      uint32_t x = __builtin_amdgcn_alignbyte(vhi[j], vlo[j], (uint32_t)(o & 3)) & own;
       float d[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {  // unconditional reads (index -1 / past the row: LDS
-        const float dr = dm_s[c + q - 1];  // words of the stage or the static area), selected
-        d[q] = (q < nown && c + q >= 1) ? dr : 0.f;
-      }
+      for (int q = 0; q < 4; ++q) d[q] = (q < nown && c + q >= 1) ? dr[4 * j + q] : 0.f;
       const int ea = a - c;  // the action's byte, if in this chunk: scatter(..., 1)
       if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
       vw[j] = x;
@@ -530,6 +542,7 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
                     logp_sel, status, epi)
     switch (greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr)) {
       case 4: CO_ROW_DISPATCH(CO_SDG, 4); break;
+      case 2: CO_SDG(CO_RL16, 16 / CO_RL16, 2); break;  // N < 4
       default: CO_ROW_DISPATCH(CO_SDG, 3);
     }
 #undef CO_SDG
@@ -603,6 +616,7 @@ extern "C" int co_cvrp_decode_step(int64_t B, int64_t Ncust, const float* logits
                     logp_sel, status, epi)
     switch (greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr)) {
       case 4: CO_ROW_DISPATCH(CO_CDG, 4); break;
+      case 2: CO_CDG(CO_RL16, 16 / CO_RL16, 2); break;  // N < 4
       default: CO_ROW_DISPATCH(CO_CDG, 3);
     }
 #undef CO_CDG

@@ -52,6 +52,7 @@ extern "C" int co_decode_step_ex(int64_t B, int64_t N, const float* logits, int6
                   logp_sel, full, status)
     switch (greedy_vw(N, lstride, logits, mask, mask, full)) {
       case 4: CO_ROW_DISPATCH(CO_GREEDY, 4); break;
+      case 2: CO_GREEDY(CO_RL16, 16 / CO_RL16, 2); break;  // N < 4
       default: CO_ROW_DISPATCH(CO_GREEDY, 3);
     }
 #undef CO_GREEDY

@@ -31,6 +31,7 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
                   ll_accum, status)
     switch (greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr)) {
       case 4: CO_ROW_DISPATCH(CO_TDG, 4); break;
+      case 2: CO_TDG(CO_RL16, 16 / CO_RL16, 2); break;  // N < 4
       default: CO_ROW_DISPATCH(CO_TDG, 3);
     }
 #undef CO_TDG

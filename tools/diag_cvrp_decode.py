@@ -20,7 +20,7 @@ from rl4co_slap_amd.envs import CVRPEnv  # noqa: E402
 from rl4co_slap_amd.td import TensorDict  # noqa: E402
 
 dev = torch.device("cuda:0")
-b, n = int(os.environ.get("B", 32768)), 100
+b, n = int(os.environ.get("B", 32768)), int(os.environ.get("N", 100))
 torch.manual_seed(1)
 la = torch.rand(b, n + 1, 2)
 dm = ((torch.rand(b, n) * 9).int() + 1).float() / 50.0
