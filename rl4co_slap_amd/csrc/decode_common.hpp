@@ -38,6 +38,7 @@ using namespace co;
 #endif
 
 __device__ __forceinline__ float co_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 // CO_DECODE_FAST (opt-in, mode flag): tanh(x) = 1 - 2 / (e^{2x} + 1) on v_exp / v_rcp (abs
 // error ~1e-7, exact +-1 saturation), the softmax exps on v_exp_f32 (<= 2 ulp) summed in
 // lane order -- log-probabilities within ~1e-6 of the reference, greedy picks exact only
@@ -81,8 +82,13 @@ __device__ __forceinline__ float row_log_sum_exp(const float (&d)[EPL], int N, i
     if constexpr ((OPT & kOptLean) != 0) {
       // every slot past N is -inf (masked) here: e^-inf = 0 needs no row-bound select;
       // the sum is >= 1 (the maximum's term), so v_log_f32 needs no denormal scaling
+      const f32x2 l2 = {1.4426950408889634f, 1.4426950408889634f};
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) s += co_exp_fast(d[k]);
+      for (int k = 0; k < EPL; k += 2) {  // the exponents' products packed, the sum in order
+        const f32x2 a = f32x2{d[k], d[k + 1]} * l2;
+        s += co_exp2(a.x);
+        s += co_exp2(a.y);
+      }
       return __builtin_amdgcn_logf(grp_sum<RL>(s)) * 0.69314718055994531f;
     }
 #pragma unroll
@@ -589,9 +595,25 @@ struct GreedyRow {
     constexpr bool kCompact = COMPACT && (OPT & kOptClip) && !(OPT & kOptFast) && CO_TANH_COMPACT;
     if constexpr (kCompact) tanh_allowed_compact(lds_row - (lane_id() / RL) * (RL * EPL));
     float m = NEG_INF, m2 = NEG_INF;
+    constexpr bool kPairs = (OPT & kOptLean) != 0 && (OPT & kOptClip) != 0 && (OPT & kOptTemp) == 0;
+    if constexpr (kPairs) {
+      // z_of<Lean> two slots at a time on packed f32 (v_pk_mul / v_pk_add / v_pk_fma: the
+      // same IEEE results as the scalar ops, at about half the issue cost per slot)
+      const f32x2 k2 = {2.8853900817779268f, 2.8853900817779268f};
+      const f32x2 one = {1.f, 1.f}, c2 = {clip, clip}, n2c = {-2.f * clip, -2.f * clip};
+#pragma unroll
+      for (int k = 0; k < EPL; k += 2) {
+        const f32x2 a = f32x2{v[k], v[k + 1]} * k2;
+        const f32x2 e = f32x2{co_exp2(a.x), co_exp2(a.y)} + one;
+        const f32x2 z = __builtin_elementwise_fma(
+            f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)}, n2c, c2);
+        v[k] = z.x;
+        v[k + 1] = z.y;
+      }
+    }
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
-      float t = kCompact ? z_scale<OPT>(v[k], clip, temp) : z_of<OPT>(v[k], clip, temp);
+      float t = kPairs ? v[k] : kCompact ? z_scale<OPT>(v[k], clip, temp) : z_of<OPT>(v[k], clip, temp);
       t = allowed(k) ? t : NEG_INF;
       v[k] = t;
       if constexpr ((OPT & kOptLean) != 0) {
@@ -672,12 +694,13 @@ struct GreedyRow {
   template <bool LEAN = false>
   __device__ __forceinline__ int select(float L, int c0, float& lp) const {
     lp = 0.f - L;
-    int idx = 0x7fffffff;
+    // the lane's first matching slot k (inline constants), c0 added once
+    constexpr int kNone = 0x40000000;
+    int kk = kNone;
 #pragma unroll
-    for (int k = EPL - 1; k >= 0; --k)
-      idx = (LEAN ? v[k] == 0.f : v[k] - L == lp) ? c0 + k : idx;
-    idx = grp_min_int<RL>(idx);
-    return idx == 0x7fffffff ? 0 : idx;  // no match only when L is NaN: all logp NaN
+    for (int k = EPL - 1; k >= 0; --k) kk = (LEAN ? v[k] == 0.f : v[k] - L == lp) ? k : kk;
+    const int idx = grp_min_int<RL>(c0 + kk);
+    return idx >= kNone ? 0 : idx;  // no match only when L is NaN: all logp NaN
   }
 };
 

@@ -318,8 +318,8 @@ struct CvrpStage {
     uint32_t cnt = 0u;
     bool feas = false;
     // every stage read first and unconditionally (index -1 / past the row: LDS words of the
-    // stage or the static area, selected below); the empty volatile asm keeps them
-    // unconditional -- else each demand read is sunk into a per-slot branch
+    // stage or the static area, whose capacity bits `cust` drops; a per-slot select of them
+    // had each demand read sunk into a branch of its own)
     float dr[EPL];
     uint32_t vlo[EPL / 4], vhi[EPL / 4];
 #pragma unroll
@@ -332,8 +332,6 @@ struct CvrpStage {
       for (int q = 0; q < 4; ++q) dr[4 * j + q] = dm_s[c + q - 1];
     }
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) asm volatile("" : "+v"(dr[k]));
-#pragma unroll
     for (int j = 0; j < EPL / 4; ++j) {
       const int c = c0 + 4 * j;
       const int nown = valid ? (NC - c < 0 ? 0 : (NC - c > 4 ? 4 : NC - c)) : 0;
@@ -343,9 +341,9 @@ struct CvrpStage {
       // v_alignbyte (reads past the row stay inside the stage / LDS; `own` masks them)
       const int o = g * NC + c;
       uint32_t x = __builtin_amdgcn_alignbyte(vhi[j], vlo[j], (uint32_t)(o & 3)) & own;
-      float d[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = (q < nown && c + q >= 1) ? dr[4 * j + q] : 0.f;
+      // the depot column's and past-the-row slots' values are whatever the stage holds:
+      // their capacity bits are dropped by `cust` below, so no select
+      const float* d = dr + 4 * j;
       const int ea = a - c;  // the action's byte, if in this chunk: scatter(..., 1)
       if (a >= 0 && ea >= 0 && ea < 4) x = (x & ~(0xffu << (8 * ea))) | (1u << (8 * ea));
       vw[j] = x;
