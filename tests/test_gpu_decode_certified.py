@@ -193,3 +193,32 @@ def test_certified_against_stock_oracle_with_clip(dev, n):
     assert int((~clear).sum()) <= 0.02 * b
     assert int((act != ref_act).sum()) <= 0.002 * b
     assert _lp_close(lp, want.gather(1, act[:, None]).squeeze(1))
+
+
+def _offset_rows(t, dev):
+    """`t` on the device as a view one element into a larger buffer: rows that start off a
+    16-byte (logits) / 4-byte (mask) boundary, so the decode takes its any-alignment path."""
+    flat = torch.empty(t.numel() + 1, dtype=t.dtype, device=dev)
+    view = flat[1:].view(t.shape)
+    view.copy_(t)
+    return view
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 6, 7, 9, 13, 101, 103])
+@pytest.mark.parametrize("misaligned", [False, True])
+def test_certified_rows_of_any_alignment_vs_oracle(dev, n, misaligned):
+    """GreedyRow's VW = 3 load (every chunk one 16-byte + one 4-byte access clamped to the
+    row's last four columns, the partial chunk shifted down; r05) and VW = 2 (N < 4): every
+    N % 4 residue, rows starting off a 16-byte boundary, tanh clipping 10 -- every action
+    the oracle's (correctly rounded tanh), logp within 1e-5; the exact math's actions too."""
+    b = 2048
+    logits, mask = _case(b, n, 300 + n)
+    want = odec.process_logits(logits.clone(), mask, 1.0, 10.0, tanh=odec.tanh_cr)
+    ref_act = odec.greedy(want, mask)
+    ref_lp = want.gather(1, ref_act[:, None]).squeeze(1)
+    lg = _offset_rows(logits, dev) if misaligned else logits.to(dev)
+    mk = _offset_rows(mask, dev) if misaligned else mask.to(dev)
+    for math in ("certified", "exact"):
+        act, lp, _ = decode_step(lg, mk, "greedy", tanh_clipping=10.0, math=math)
+        assert torch.equal(act.cpu(), ref_act), math
+        assert _lp_close(lp.cpu(), ref_lp), math
