@@ -119,8 +119,8 @@ __global__ __launch_bounds__(256) void pomo_baseline_kernel(int64_t B, int S, co
 // The decode loop's epilogue on step-major rows: a 256-thread workgroup owns 64 instances
 // (columns b0 .. b0+63 of the step rows) and walks the steps in chunks of kStackChunk:
 // the chunk's action / log-probability rows are loaded coalesced (a wave reads one step's
-// 64 values) into LDS, then written out transposed -- each instance's chunk of its
-// [B, T] rows as 4 threads x 8 consecutive values -- while thread b sums its row's
+// 64 values) into LDS, then written out transposed -- consecutive threads on consecutive
+// steps of an instance's [B, T] row -- while thread b sums its row's
 // log-probabilities in step order in f64 (ll) and tests `> -1000` (decoding.py:57-58).
 constexpr int kStackChunk = 32;
 
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void episode_stack_kernel(
     int64_t B, int64_t T, const int64_t* __restrict__ act_sm, int64_t act_rs,
     const float* __restrict__ logp_sm, int64_t logp_rs, int64_t* __restrict__ actions,
     float* __restrict__ logprobs, float* __restrict__ ll, int32_t* status) {
-  __shared__ int64_t s_act[kStackChunk][64];
+  __shared__ int64_t s_act[kStackChunk][65];  // +1: the stores read down a column too
   __shared__ float s_lp[kStackChunk][65];  // +1: the row-wise sum reads down a column
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int64_t b0 = (int64_t)blockIdx.x * 64;
@@ -144,23 +144,31 @@ __global__ __launch_bounds__(256) void episode_stack_kernel(
       }
     }
     __syncthreads();
-    // transposed stores: row r = tid / 4, its values j = (tid % 4) * 8 .. + 7 of the chunk
-    const int r = tid >> 2, j0 = (tid & 3) * 8;
-    if (r < nb) {
-      const int64_t ob = (b0 + r) * T + t0;
-#pragma unroll
-      for (int j = j0; j < j0 + 8; ++j) {
-        if (j < nt) {
-          if (actions) actions[ob + j] = s_act[j][r];
-          if (logprobs) logprobs[ob + j] = s_lp[j][r];
-        }
-      }
+    // transposed stores: element i of the chunk's 64 x nt output block is row i / nt, step
+    // i % nt, so consecutive threads write consecutive addresses of a row (r05: 4 threads
+    // x 8 values per row left every store instruction 64 separate 8-byte pieces)
+    for (int i = tid; i < nb * nt; i += 256) {
+      const int r = i / nt, j = i - r * nt;
+      const int64_t o = (b0 + r) * T + t0 + j;
+      if (actions) actions[o] = s_act[j][r];
+      if (logprobs) logprobs[o] = s_lp[j][r];
     }
     if (logp_sm && tid < nb) {  // thread b: its row, in step order
-      for (int j = 0; j < nt; ++j) {
-        const float v = s_lp[j][tid];
-        acc += (double)v;
-        bad |= !(v > -1000.f);
+      if (nt == kStackChunk) {
+        float v[kStackChunk];
+#pragma unroll
+        for (int j = 0; j < kStackChunk; ++j) v[j] = s_lp[j][tid];  // reads ahead of the chain
+#pragma unroll
+        for (int j = 0; j < kStackChunk; ++j) {
+          acc += (double)v[j];
+          bad |= !(v[j] > -1000.f);
+        }
+      } else {
+        for (int j = 0; j < nt; ++j) {
+          const float v = s_lp[j][tid];
+          acc += (double)v;
+          bad |= !(v > -1000.f);
+        }
       }
     }
     __syncthreads();  // the next chunk overwrites the tile
