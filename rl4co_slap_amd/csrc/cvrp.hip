@@ -790,12 +790,35 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
     // lane m-1 (shuffle) or, for lane 0, from the previous block's lane 63 (depot at m = 0)
     int a_carry = 0;
     float px_carry = lrow[0].x, py_carry = lrow[0].y;
-    for (int base = 0; base < M; base += 64) {  // wave-uniform trip count (ballot below)
+    // kPre 64-step pieces at a time: their action loads issued together, then their
+    // coordinate / demand gathers together (r05: one piece per iteration waited for two
+    // dependent round trips per 64 steps -- 8 for T = 199)
+    constexpr int kPre = 4;
+    for (int base0 = 0; base0 < M; base0 += 64 * kPre) {
+    int64_t a_pre[kPre];
+    float2 q_pre[kPre];
+    float d_pre[kPre];
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int m = base0 + 64 * u + lane;
+      a_pre[u] = (m < T) ? arow[(int64_t)m * st] : 0;  // m == T: back to the depot
+    }
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+      const int m = base0 + 64 * u + lane;
+      const int a32 = a_pre[u] >= 0 && a_pre[u] <= N ? (int)a_pre[u] : 0;
+      q_pre[u] = lrow[m < M ? a32 : 0];
+      d_pre[u] = check ? demand[b * (int64_t)N + (a32 > 0 ? a32 - 1 : 0)] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {  // wave-uniform trip count (ballot below)
+      const int base = base0 + 64 * u;
+      if (base >= M) break;
       const int m = base + lane;
-      const int64_t a_to = (m < T) ? arow[(int64_t)m * st] : 0;  // m == T: back to the depot
+      const int64_t a_to = a_pre[u];
       const bool ok_to = a_to >= 0 && a_to <= N;
       const int a32 = ok_to ? (int)a_to : -1;
-      const float2 q = lrow[ok_to && m < M ? a32 : 0];
+      const float2 q = q_pre[u];
       int a_from = __shfl_up(a32, 1, 64);
       float px = __shfl_up(q.x, 1, 64), py = __shfl_up(q.y, 1, 64);
       if (lane == 0) {
@@ -824,7 +847,7 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
               const uint32_t bit = 1u << (a & 31);
               if (atomicOr(&bits[a >> 5], bit) & bit) bad = true;
             }
-            dseq[m] = (a == 0) ? -cap : demand[b * (int64_t)N + a - 1];
+            dseq[m] = (a == 0) ? -cap : d_pre[u];
           }
         }
       }
@@ -836,6 +859,7 @@ __global__ __launch_bounds__(WAVES * 64) void cvrp_reward_kernel(
         nseg += __popcll(bal);
         start_here = false;
       }
+    }
     }
     acc = wave_sum(acc);
     if (lane == 0) reward[b] = -(float)acc;

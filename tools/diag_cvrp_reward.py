@@ -44,6 +44,22 @@ for check in (1, 0):
     e1.record()
     torch.cuda.synchronize(dev)
     out[f"check{check}_us"] = e0.elapsed_time(e1) * 1e3 / 30
+# the drop-in loop's layout: row-major [B, T] actions (cvrp_reward_kernel, wave per instance)
+ref = ep.reward.clone()
+acts_rm = acts.t().contiguous()
+rew_rm = torch.empty_like(ep.reward)
+f = nat.bind("co_cvrp_reward", b, n, T, nat.ptr(ep.locs), nat.ptr(acts_rm), T, 1,
+             nat.ptr(ep.demand), nat.ptr(ep.vcap_t), 1, nat.ptr(rew_rm), nat.ptr(ep.status))
+for _ in range(3):
+    f(s)
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(30):
+    f(s)
+e1.record()
+torch.cuda.synchronize(dev)
+out["rowmajor_check1_us"] = e0.elapsed_time(e1) * 1e3 / 30
+out["rowmajor_close"] = bool(torch.allclose(rew_rm, ref, rtol=1e-6, atol=0)) and int(ep.status.item()) == 0
 print(json.dumps(out))
 if os.environ.get("CO_TIMING"):  # a -DCO_CVRPR_TIMING build: per-workgroup phase clocks
     f = nat.bind("co_cvrp_reward", b, n, T, nat.ptr(ep.locs), nat.ptr(acts), 1, b,
