@@ -119,7 +119,8 @@ __global__ __launch_bounds__(256) void pomo_baseline_kernel(int64_t B, int S, co
 // The decode loop's epilogue on step-major rows: a 256-thread workgroup owns 64 instances
 // (columns b0 .. b0+63 of the step rows) and walks the steps in chunks of kStackChunk:
 // the chunk's action / log-probability rows are loaded coalesced (a wave reads one step's
-// 64 values) into LDS, then written out transposed -- consecutive threads on consecutive
+// 64 values; the next chunk's loads in flight during this chunk's stores) into LDS, then
+// written out transposed -- consecutive threads on consecutive
 // steps of an instance's [B, T] row -- while thread b sums its row's
 // log-probabilities in step order in f64 (ll) and tests `> -1000` (decoding.py:57-58).
 constexpr int kStackChunk = 32;
@@ -135,15 +136,34 @@ __global__ __launch_bounds__(256) void episode_stack_kernel(
   const int nb = (int)(B - b0 < 64 ? B - b0 : 64);
   double acc = 0.0;
   bool bad = false;
+  // wave w loads steps w, w + 4, ... of a chunk into registers (one coalesced row piece
+  // each; indices clamped into the rows, so every load is unconditional); the next chunk's
+  // loads are issued before this chunk's stores, so they are in flight while it stores
+  constexpr int KW = kStackChunk / 4;
+  int64_t ra[KW];
+  float rl[KW];
+  const int64_t bb = b0 + (lane < nb ? lane : nb - 1);
+  auto fetch = [&](int64_t t0) {
+#pragma unroll
+    for (int i = 0; i < KW; ++i) {
+      const int64_t tt = t0 + w + 4 * i < T ? t0 + w + 4 * i : T - 1;
+      if (act_sm) ra[i] = act_sm[tt * act_rs + bb];
+      if (logp_sm) rl[i] = logp_sm[tt * logp_rs + bb];
+    }
+  };
+  fetch(0);
   for (int64_t t0 = 0; t0 < T; t0 += kStackChunk) {
     const int nt = (int)(T - t0 < kStackChunk ? T - t0 : kStackChunk);
-    for (int k = w; k < nt; k += 4) {  // step t0 + k: one coalesced row piece per wave
-      if (lane < nb) {
-        if (act_sm) s_act[k][lane] = act_sm[(t0 + k) * act_rs + b0 + lane];
-        if (logp_sm) s_lp[k][lane] = logp_sm[(t0 + k) * logp_rs + b0 + lane];
+#pragma unroll
+    for (int i = 0; i < KW; ++i) {
+      const int k = w + 4 * i;
+      if (k < nt && lane < nb) {
+        if (act_sm) s_act[k][lane] = ra[i];
+        if (logp_sm) s_lp[k][lane] = rl[i];
       }
     }
     __syncthreads();
+    if (t0 + kStackChunk < T) fetch(t0 + kStackChunk);
     // transposed stores: element i of the chunk's 64 x nt output block is row i / nt, step
     // i % nt, so consecutive threads write consecutive addresses of a row (r05: 4 threads
     // x 8 values per row left every store instruction 64 separate 8-byte pieces)
