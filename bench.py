@@ -307,11 +307,21 @@ def cpu_threads():
     return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
 
 
-def _spread(times, work):
-    """min / median / max rate over the timed episodes (the first, a warm-up, dropped)."""
+def _loadavg():
+    try:
+        return [round(x, 2) for x in os.getloadavg()]
+    except OSError:
+        return None
+
+
+def _spread(times, work, load_before=None):
+    """min / median / max rate over the timed episodes (the first, a warm-up, dropped), and
+    the host's load average (1 / 5 / 15 min) before and after them: a CPU baseline taken
+    on a loaded host reads low, and the driver's records should show it."""
     ts = sorted(times[1:])
     return {"value": work / ts[len(ts) // 2], "value_min": work / ts[-1], "value_max": work / ts[0],
-            "episodes": len(ts)}
+            "episodes": len(ts), "host_loadavg_before": load_before,
+            "host_loadavg_after": _loadavg()}
 
 
 def host_cpu():
@@ -348,14 +358,14 @@ def cpu_baseline_tsp(locs, acts, episodes=5):
     torch.set_num_threads(threads)
     b, n = acts.shape
     env = TSPOracle(num_loc=n, seed=1234)
-    times = []
+    times, load0 = [], _loadavg()
     for _ in range(episodes + 1):
         td = env.reset(TD({"locs": locs}, [b]))
         it = iter(range(n))
         t0 = time.perf_counter()
         rollout(env, td, lambda td: acts[:, next(it)])
         times.append(time.perf_counter() - t0)
-    return {**_spread(times, b * n), "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {**_spread(times, b * n, load0), "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle (CPU PyTorch restatement) TSP-{n} teacher-forced rollout: reset + "
                       f"{n} x _step + get_reward with the double validity sort, B={b} (the full "
                       f"GPU workload), median (min / max beside it) of {episodes} episodes after "
@@ -386,13 +396,13 @@ def cpu_baseline_slap(b=16384, episodes=5):
     gen["freq"] = env.freq_sampler.sample((b, env.n_products, 1))
     gen["picklist"] = env.picklist([b])
     gen = TD(gen, [b])
-    times = []
+    times, load0 = [], _loadavg()
     for _ in range(episodes + 1):
         td = env.reset(TD({k: v.clone() for k, v in gen.items()}, [b]))
         t0 = time.perf_counter()
         rollout(env, td, slap_closest_free_action)
         times.append(time.perf_counter() - t0)
-    return {**_spread(times, b * 20), "unit": "env-steps/s", "cores": cpu_threads(),
+    return {**_spread(times, b * 20, load0), "unit": "env-steps/s", "cores": cpu_threads(),
             "kind": "port",
             "sample": f"oracle SLAP rollout (closest-free policy, per-batch Python loop of "
                       f"slap/env.py:61-62 kept), B={b}, median (min / max) of {episodes} "
@@ -412,7 +422,7 @@ def cpu_baseline_cvrp(b=32768, n=100, episodes=5):
     locs_all = torch.rand(b, n + 1, 2)
     demand = ((torch.rand(b, n) * 9).int() + 1).float() / 50.0
     env = CVRPOracle(num_loc=n, seed=1234)
-    times, steps = [], 0
+    times, steps, load0 = [], 0, _loadavg()
     for _ in range(episodes + 1):
         td = env.reset(TD({"depot": locs_all[:, 0].clone(), "locs": locs_all[:, 1:].clone(),
                            "demand": demand.clone(),
@@ -421,7 +431,7 @@ def cpu_baseline_cvrp(b=32768, n=100, episodes=5):
         _, _, acts = rollout(env, td, cvrp_nearest_action)
         times.append(time.perf_counter() - t0)
         steps = acts.shape[1]
-    return {**_spread(times, b * steps), "unit": "env-steps/s", "cores": threads,
+    return {**_spread(times, b * steps, load0), "unit": "env-steps/s", "cores": threads,
             "kind": "port",
             "sample": f"oracle CVRP-{n} rollout, nearest-feasible policy, B={b} (config 3, the "
                       f"GPU batch), T={steps} steps, get_reward with the validity + capacity "
@@ -446,7 +456,7 @@ def cpu_baseline_pomo(b=256, n=100, episodes=5):
     locs = torch.rand(b, n, 2, generator=g)
     logits = torch.randn(n - 1, n * b, n, generator=g)
     env = TSPOracle(num_loc=n, seed=1234)
-    times = []
+    times, load0 = [], _loadavg()
     for _ in range(episodes + 1):
         td = env.reset(TD({"locs": locs.clone()}, [b]))
         it = iter(range(n - 1))
@@ -455,7 +465,7 @@ def cpu_baseline_pomo(b=256, n=100, episodes=5):
                                    decode_type="multistart_greedy", tanh_clipping=10.0)
         pomo_loss(out["reward"], out["log_likelihood"], n)
         times.append(time.perf_counter() - t0)
-    return {**_spread(times, b * n * n), "unit": "env-steps/s", "cores": threads, "kind": "port",
+    return {**_spread(times, b * n * n, load0), "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle POMO TSP-{n} episode: constructive_forward multistart greedy "
                       f"(batchify x {n} starts, start step + {n - 1} decode steps, tanh clip 10, "
                       f"fixed step-major logits) + reward with validity + shared-baseline loss, "
@@ -657,6 +667,26 @@ def main():
         dist.destroy_process_group()
 
 
+def pmc_sq_issue(target, kernel):
+    """(SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES, file) of `target`'s main kernel from the newest
+    committed profiles/r*_pmc_sq.txt (scripts/gpu_pmc_sq.sh), or None."""
+    import glob
+    import re
+
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_sq.txt")), reverse=True):
+        try:
+            lines = open(f).read().splitlines()
+        except OSError:
+            continue
+        for i, line in enumerate(lines[:-1]):
+            w = line.split()
+            if len(w) >= 2 and w[0] == target and w[1].startswith(kernel):
+                m = re.search(r"\bactive=([0-9.eE+-]+)", lines[i + 1])
+                if m:
+                    return float(m.group(1)), os.path.basename(f)
+    return None
+
+
 def summarize(out):
     """The figures a reader needs first, in one short record: every per-GPU rate with its
     HBM fraction, the drop-in loops' launches / GPU / host time per step."""
@@ -674,6 +704,14 @@ def summarize(out):
                                    "frac": r(t["roofline"]["frac"])}
         sm["slap_b65536_stepwise"] = {"env_steps_s": r(t["stepwise"]["value"], 0),
                                       "frac_wall": r(t["stepwise"]["frac_wall"])}
+    # the same run's streaming ceiling (co_probe_copy of 2 GiB): each rate below also as a
+    # fraction of it, so a box that streams slower shows up here, not as a regression
+    cp = out["roofline"].get("copy_probe", {})
+    copy_gbs = cp.get("2GiB", {}).get("GBps")
+    sm["copy_GBps"] = r(copy_gbs, 1)
+    sm["copy_same_bytes_GBps"] = r(cp.get("same_bytes", {}).get("GBps"), 1)
+    foc = lambda gbs: r(gbs / copy_gbs) if gbs and copy_gbs else None  # noqa: E731
+    sm["tsp100_fused_final_state"]["frac_of_copy"] = foc(out["roofline"]["achieved"])
     modes = out.get("modes", {})
     for name in ("dropin_tsp100", "dropin_cvrp100", "dropin_slap_b16384", "dropin_slap_b65536"):
         m = modes.get(name)
@@ -688,12 +726,14 @@ def summarize(out):
                     "host_us_per_step_b64_all_in": r(m.get("host_us_per_step_b64"), 2),
                     "host_us_per_loop_step_b64": r(m.get("host_us_per_loop_step_b64"), 2),
                     "decode_fused_kernel_us": r(m.get("decode_fused_kernel_us"), 2),
-                    "hbm_frac": r(m.get("hbm_frac"))}
+                    "hbm_frac": r(m.get("hbm_frac")),
+                    "frac_of_copy": foc(m.get("achieved_GBps_per_gpu"))}
     for name in ("pomo_tsp100", "tsp_fused_nearest", "cvrp_fused_nearest", "cvrp_stepwise_graph"):
         m = modes.get(name)
         if m:
             sm[name] = {"env_steps_s": r(m["value"], 0), "ms_per_episode": r(m["ms_per_episode"]),
-                        "hbm_frac": r(m.get("hbm_frac"))}
+                        "hbm_frac": r(m.get("hbm_frac")),
+                        "frac_of_copy": foc(m.get("achieved_GBps_per_gpu"))}
     sk = out.get("step_kernels_vs_copy", {})
     if sk:
         sm["step_kernels_frac_of_copy"] = {k2: r(v["frac_of_copy"]) for k2, v in sk.items()}
@@ -701,7 +741,15 @@ def summarize(out):
         c = out.get(name)
         if c:
             sm[name] = {"value": r(c["value"], 0), "min": r(c.get("value_min"), 0),
-                        "max": r(c.get("value_max"), 0), "threads": c["cores"]}
+                        "max": r(c.get("value_max"), 0), "threads": c["cores"],
+                        "loadavg_1m": [(c.get("host_loadavg_before") or [None])[0],
+                                       (c.get("host_loadavg_after") or [None])[0]]}
+    # every other rate with an HBM fraction: the same fraction of this run's copy ceiling
+    for v in sm.values():
+        if isinstance(v, dict) and "frac_of_copy" not in v and copy_gbs:
+            f = v.get("hbm_frac", v.get("frac", v.get("frac_wall")))
+            if f is not None:
+                v["frac_of_copy"] = r(f * HBM_PEAK_GBS / copy_gbs)
     return sm
 
 
@@ -805,7 +853,10 @@ def annotate_modes(modes, n, world):
             m = modes[name]
             tf = m["value"] / world * cand * 5 / 1e12
             m.update({"bound": "valu-issue (instructions per instance-step; not HBM)",
-                      "achieved_TFLOPs_per_gpu": tf, "valu_frac": tf / FP32_VECTOR_PEAK_TFS})
+                      "distance_TFLOPs_per_gpu": tf})
+            sq = pmc_sq_issue(name, name.split("_")[0] + "_nearest_lds_kernel")
+            if sq is not None:  # issuing fraction of wave cycles, from the committed SQ pass
+                m["sq_issue_frac"], m["sq_issue_source"] = sq
 
 
 def bench_slap(b, k, world, rank, dev, stepwise=True):

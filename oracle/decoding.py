@@ -38,6 +38,9 @@ def process_logits(logits, mask=None, temperature=1.0, tanh_clipping=0.0, mask_l
         logits = tanh(logits) * tanh_clipping
     if mask_logits:
         assert mask is not None, "mask must be provided if mask_logits is True"
+        # the reference writes -inf into the tensor it was given (with tanh_clipping == 0
+        # that is the caller's logits, decoding.py:178); the product does not,
+        # so the restatement works on a copy and returns the same log-probabilities
         logits = logits.clone()
         logits[~mask] = float("-inf")
     logits = logits / temperature

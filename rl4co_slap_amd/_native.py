@@ -19,6 +19,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libco_env.so")
+_PRODUCT_LIB_PATH = LIB_PATH
 
 _i64, _i32, _f32, _u64, _p = ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p
 _f64 = ctypes.c_double
@@ -112,9 +113,15 @@ def load():
         lib.co_build_info.restype = ctypes.c_char_p
         lib.co_build_info.argtypes = []
         if hasattr(lib, "co_variant_timing_cut") or hasattr(lib, "co_variant_timing_cut_decode"):
-            warnings.warn(f"rl4co_slap_amd: {LIB_PATH} is a timing-cut diagnostic build "
-                          "(CO_CVRP_CUT / CO_CVRP_RCUT): its results and status bits are not "
-                          "valid", RuntimeWarning, stacklevel=2)
+            # a diagnostic build (csrc/co_diag.hpp: CO_DIAG_* / CO_CVRP_CUT / CO_CVRP_RCUT):
+            # its results and status bits are wrong by design.  In the product's slot it is
+            # refused; a measurement tool that points LIB_PATH at a variant (or sets
+            # CO_ALLOW_DIAG_LIB=1) gets a warning.
+            msg = (f"rl4co_slap_amd: {LIB_PATH} is a diagnostic build (timing cut / counting "
+                   "variant): its results and status bits are not valid")
+            if LIB_PATH == _PRODUCT_LIB_PATH and not os.environ.get("CO_ALLOW_DIAG_LIB"):
+                raise NativeUnavailable(msg + "; rebuild with `python -m rl4co_slap_amd.csrc.build`")
+            warnings.warn(msg, RuntimeWarning, stacklevel=2)
         _lib = lib
         return lib
 
@@ -317,6 +324,8 @@ class _TorchStep:
         self.episode_stack = bound(mod.episode_stack, "co_episode_stack")
         self.slab_fresh = mod.slab_fresh
         self.clear_pool = mod.clear_pool
+        self.set_inplace = mod.set_inplace
+        self.inplace_policy = mod.inplace_policy
 
 
 def torchstep():

@@ -4,7 +4,8 @@
 // compile-time false and the compiler drops the code it guards.  Tools build variants of
 // the library with one switch set (tools/build_variants.sh, tools/diag_cert_count.py) to
 // time or count one part of a kernel; such a library exports co_variant_timing_cut_decode
-// and _native.load() refuses it for anything but that tool.
+// (decode_step.hip, for any of the switches below), and _native.load() refuses it in the
+// product's slot (_lib/libco_env.so) and only warns when a tool points LIB_PATH at it.
 #pragma once
 
 namespace co {

@@ -10,6 +10,8 @@
 #pragma once
 // Shared by decode_step.hip (co_decode_step[_ex], beam search) and decode_tsp.hip
 // (co_tsp_decode_step): two translation units, compiled in parallel.
+#include <type_traits>
+
 #include "co_common.hpp"
 #include "co_diag.hpp"
 #include "co_math.hpp"
@@ -439,6 +441,20 @@ __device__ __forceinline__ float lane_select(bool c, float t, float f) {
   return r;
 }
 
+#ifndef CO_DECODE_NT
+#define CO_DECODE_NT 0  // logits chunks by non-temporal loads (read once per step)
+#endif
+template <class F>
+__device__ __forceinline__ F ld_logit4(const F* p) {
+  if constexpr (CO_DECODE_NT && std::is_same<F, float4>::value) {
+    return ld_s<true>(p);
+  } else if constexpr (CO_DECODE_NT) {
+    return __builtin_nontemporal_load(p);
+  } else {
+    return *p;
+  }
+}
+
 template <int RL, int EPL, int VW>
 struct GreedyRow {
   static_assert(EPL % 4 == 0, "GreedyRow keeps the mask in u32 words");
@@ -460,7 +476,7 @@ struct GreedyRow {
       uint32_t m = 0u;
       float xf[4] = {0.f, 0.f, 0.f, 0.f};
       if (valid && c + 4 <= N) {
-        const F x = *reinterpret_cast<const F*>(lrow + c);
+        const F x = ld_logit4(reinterpret_cast<const F*>(lrow + c));
         xf[0] = x[0];
         xf[1] = x[1];
         xf[2] = x[2];
@@ -497,7 +513,7 @@ struct GreedyRow {
     for (int j = 0; j < EPL / 4; ++j) {  // every load issued before the first use
       const int c = c0 + 4 * j;
       const int cb = c < N - 4 ? c : N - 4;
-      x[j] = *reinterpret_cast<const F*>(lrow + cb);
+      x[j] = ld_logit4(reinterpret_cast<const F*>(lrow + cb));
       w[j] = mrow ? (uint32_t) * reinterpret_cast<const M*>(mrow + cb) : 0x01010101u;
     }
 #pragma unroll

@@ -3,8 +3,10 @@
 // ranking.
 #include "decode_common.hpp"
 
-#if defined(CO_DIAG_FASTTANH) || defined(CO_DIAG_FASTEXP)  // co_diag.hpp: kDiagTimingCut
-// timing-diagnostic build: the "exact" decode is not exact (see _native.load())
+#if defined(CO_DIAG_FASTTANH) || defined(CO_DIAG_FASTEXP) || defined(CO_DIAG_CVRP_CUT) || \
+    defined(CO_DIAG_CERT_COUNT)  // co_diag.hpp: kDiagTimingCut || kDiagCertCount
+// diagnostic build: the "exact" decode is not exact, the CVRP decode step lacks its decode
+// or transition, or certified rows carry marker log-probabilities (see _native.load())
 extern "C" __attribute__((visibility("default"))) const int co_variant_timing_cut_decode = 1;
 #endif
 

@@ -426,10 +426,21 @@ extern "C" int co_uniform_fill(float* out, int64_t n, float low, float high, flo
 namespace {
 // one 16-B unit per thread over a full grid (the float4-copy shape of the guide's 6.29 TB/s
 // measurement; grid-stride variants with 1 or 4 units in flight measured 5.07 / 4.25 TB/s)
+#ifndef CO_PROBE_NT
+#define CO_PROBE_NT 1  // non-temporal loads and stores (r06: 2 GiB 6.2 -> 6.6 TB/s, the best copy)
+#endif
 __global__ __launch_bounds__(256) void probe_copy_kernel(const uint4* __restrict__ src,
                                                          uint4* __restrict__ dst, int64_t n16) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n16) dst[i] = src[i];
+  if (i < n16) {
+    if (CO_PROBE_NT) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(
+          __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + i),
+          reinterpret_cast<u32x4*>(dst) + i);
+    } else
+      dst[i] = src[i];
+  }
 }
 }  // namespace
 

@@ -17,6 +17,7 @@
 #include <torch/csrc/autograd/python_variable.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -160,17 +161,23 @@ struct StatePool {
 // (episode_stack -> co_episode_stack) transposes in one launch instead of two
 // torch.stack calls.  slab_fresh(steps) makes the next take start a new storage sized for
 // an episode of that many steps, so an episode does not straddle two storages.
+// The slab remembers the stream its rows were last handed out on: rewriting it from the
+// top is safe only in that stream's order (kernels that read the last episode's rows --
+// the epilogue, a reward, a caller's own launch -- were queued there), so an episode start
+// on another stream takes a new storage, as StatePool::acquire does.
 struct Slab {
   static constexpr int64_t kSteps = 64;
   c10::Device dev{c10::DeviceType::CPU};
   c10::Storage st;
+  void* stream = nullptr;
   int64_t off = 0, cap = 0, fresh_steps = 0;
-  // a region of nbytes (a multiple of kAlign): offset into `st`
-  int64_t take(const c10::Device& d, int64_t nbytes) {
-    if (fresh_steps > 0 && st && d == dev && st.use_count() == 1 &&
+  // a region of nbytes (a multiple of kAlign) for a launch on stream s: offset into `st`
+  int64_t take(const c10::Device& d, int64_t nbytes, void* s) {
+    if (fresh_steps > 0 && st && d == dev && s == stream && st.use_count() == 1 &&
         nbytes * fresh_steps <= (int64_t)st.nbytes()) {
       // an episode start on a slab nothing refers to any more (the last episode's row
-      // views are gone): rewrite it from the top, in stream order, instead of allocating
+      // views are gone), on the stream that used it: rewrite it from the top, in stream
+      // order, instead of allocating
       cap = (int64_t)st.nbytes();
       fresh_steps = 0;
       off = 0;
@@ -181,6 +188,7 @@ struct Slab {
       dev = d;
       off = 0;
     }
+    stream = s;
     const int64_t o = off;
     off += nbytes;
     return o;
@@ -220,13 +228,13 @@ int tsp_launch(TspDecodeStep fn, const at::Tensor& logits, const at::Tensor& mas
   if (!take && (!first || !fits(*first, dev, at::kLong, b))) return -1;
   if (ain && !fits(*ain, dev, at::kLong, b)) return -1;
   const int64_t kb = up(8 * b);
-  const int64_t ko = g_slab.take(dev, 2 * kb);
+  void* stream = current_stream(dev);
+  const int64_t ko = g_slab.take(dev, 2 * kb, stream);
   out[0] = view_of(g_slab.st, at::kLong, ko, {b});
   out[1] = view_of(g_slab.st, at::kFloat, ko + kb, {b});
   Carver c;
   const int64_t om = c.take(b * nl), oi = c.take(8 * b), of = c.take(8 * b), od = c.take(b),
                 orw = c.take(b);
-  void* stream = current_stream(dev);
   const c10::Storage st = g_state.acquire(dev, c.off, stream);
   out[2] = view_of(st, at::kBool, om, {b, nl});
   out[3] = view_of(st, at::kLong, oi, i.sizes());
@@ -462,8 +470,22 @@ inline int set_wrapped(PyObject* td, const char* k, at::Tensor& t) {
 // True when `o` (a tensor the td dict holds) is referenced by nothing but that dict: one
 // Python reference, one at::Tensor handle, a storage of its own (no views, no pool), no
 // autograd.  Writing it in place then cannot be told apart from writing a fresh copy.
+// The reference-count test is CPython behaviour this module was built and tested on
+// (3.10, with the GIL): a free-threaded build defers and biases reference counts, and
+// immortal objects (3.12+) report fixed counts, so there the in-place writes are off at
+// compile time and every step takes fresh storages.  CO_NO_INPLACE=1 (read at import) or
+// set_inplace(False) turns them off at run time.
+#if defined(Py_GIL_DISABLED) || PY_VERSION_HEX >= 0x030C0000
+constexpr bool kInplaceBuild = false;
+#else
+constexpr bool kInplaceBuild = true;
+#endif
+bool g_inplace = kInplaceBuild;
+// the stream of the last slap_reset_td / slap_step_td launch (none yet: a value no stream has)
+void* g_slap_stream = reinterpret_cast<void*>(~uintptr_t(0));
+
 inline bool exclusively_held(PyObject* o, const at::Tensor& t) {
-  return Py_REFCNT(o) == 1 && t.use_count() == 1 && t.storage().use_count() == 1 &&
+  return g_inplace && Py_REFCNT(o) == 1 && t.use_count() == 1 && t.storage().use_count() == 1 &&
          !t.requires_grad() && t.is_contiguous() && t.storage_offset() == 0;
 }
 
@@ -486,6 +508,7 @@ struct SlapBlock {
   }
   bool held_alone(PyObject* const (&o)[4], const at::Tensor* const (&t)[4], int64_t b,
                   int64_t l) const {
+    if (!g_inplace) return false;
     const c10::StorageImpl* sti = t[0]->storage().unsafeGetStorageImpl();
     if (t[0]->storage().use_count() != 4 || t[0]->storage().nbytes() != (size_t)nbytes) return false;
     const int64_t offs[4] = {om, oi / 8, od, orw};
@@ -568,19 +591,23 @@ PyObject* slap_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     if (ain && !fits(*ain, dev, at::kLong, b)) Py_RETURN_NONE;
     // the untouched arange: to_choose[:, 0] == k in every row (k + remaining columns == P)
     const bool uniform = ktc >= 0 && ktc < p && ktc + tc.size(1) == p;
-    const bool asg_here = exclusively_held(as_o, asg);
+    void* stream = current_stream(dev);
+    // in place only in the stream order of the previous step's launch (which made the
+    // tensors or last read them)
+    const bool same_stream = stream == g_slap_stream;
+    g_slap_stream = stream;
+    const bool asg_here = same_stream && exclusively_held(as_o, asg);
     const SlapBlock blk(b, l);
     bool blk_here = false;
-    if (dn_o && rw_o) {
+    if (same_stream && dn_o && rw_o) {
       PyObject* const os[4] = {mask_o, i_o, dn_o, rw_o};
       const at::Tensor* const ts[4] = {&mask, &i, &THPVariable_Unpack(dn_o), &THPVariable_Unpack(rw_o)};
       blk_here = blk.held_alone(os, ts, b, l);
     }
     const int64_t kb = up(8 * b);
-    const int64_t ko = g_slab.take(dev, 2 * kb);
+    const int64_t ko = g_slab.take(dev, 2 * kb, stream);
     at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
     at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b});
-    void* stream = current_stream(dev);
     at::Tensor asg_out = asg_here ? asg : view_of(new_storage(dev, 4 * b * p), at::kInt, 0,
                                                   asg.sizes());
     at::Tensor mask_out, i_out, done, reward;
@@ -708,13 +735,13 @@ PyObject* cvrp_step_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
       Py_RETURN_NONE;
     if (ain && !fits(*ain, dev, at::kLong, b)) Py_RETURN_NONE;
     const int64_t kb = up(8 * b);
-    const int64_t ko = g_slab.take(dev, 2 * kb);
+    void* stream = current_stream(dev);
+    const int64_t ko = g_slab.take(dev, 2 * kb, stream);
     at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
     at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b});
     Carver c;
     const int64_t ou = c.take(4 * b), ov = c.take(b * (nl + 1)), oc = c.take(8 * b),
                   od = c.take(b), orw = c.take(b), om = c.take(b * (nl + 1));
-    void* stream = current_stream(dev);
     const c10::Storage st = g_state.acquire(dev, c.off, stream);
     at::Tensor used_out = view_of(st, at::kFloat, ou, used.sizes());
     at::Tensor vis_out = view_of(st, at::kByte, ov, vis.sizes());
@@ -791,11 +818,11 @@ PyObject* decode_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
   }
   try {
     const int64_t kb = up(8 * b);
-    const int64_t ko = g_slab.take(dev, 2 * kb);
+    void* stream = current_stream(dev);
+    const int64_t ko = g_slab.take(dev, 2 * kb, stream);
     at::Tensor act = view_of(g_slab.st, at::kLong, ko, {b});
     at::Tensor logp = view_of(g_slab.st, at::kFloat, ko + kb, {b}), full;
     if (want_full) full = at::empty({b, nl}, logits.options());
-    void* stream = current_stream(dev);
     int rc;
     Py_BEGIN_ALLOW_THREADS
     rc = fn(b, nl, logits.const_data_ptr<float>(), logits.stride(0),
@@ -1004,6 +1031,7 @@ PyObject* slap_reset_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
     at::Tensor done = view_of(st, at::kBool, od, {b, 1});
     at::Tensor term = view_of(st, at::kBool, oe, {b, 1});
     void* stream = current_stream(dev);
+    g_slap_stream = stream;  // the episode's tensors are made in this stream's order
     int rc;
     Py_BEGIN_ALLOW_THREADS
     rc = fn(b, l, p, static_cast<uint8_t*>(mask.mutable_data_ptr()), tc.mutable_data_ptr<float>(),
@@ -1032,6 +1060,23 @@ PyObject* slap_reset_td(PyObject*, PyObject* const* a, Py_ssize_t n) {
   }
 }
 
+// set_inplace(flag) -> previous flag: allow the in-place state writes (only where the
+// build allows them: kInplaceBuild); inplace_policy() -> (build allows, enabled)
+PyObject* set_inplace(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 1) {
+    PyErr_SetString(PyExc_TypeError, "set_inplace: 1 argument");
+    return nullptr;
+  }
+  const int v = PyObject_IsTrue(a[0]);
+  if (v < 0) return nullptr;
+  const bool prev = g_inplace;
+  g_inplace = kInplaceBuild && v;
+  return PyBool_FromLong(prev);
+}
+PyObject* inplace_policy(PyObject*, PyObject* const*, Py_ssize_t) {
+  return Py_BuildValue("(OO)", kInplaceBuild ? Py_True : Py_False, g_inplace ? Py_True : Py_False);
+}
+
 // clear_pool() -> None: drop every pooled state storage (tensors still held stay valid)
 PyObject* clear_pool(PyObject*, PyObject* const*, Py_ssize_t) {
   g_state.clear();
@@ -1043,6 +1088,11 @@ PyMethodDef methods[] = {
      METH_FASTCALL, "SLAPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
     {"cvrp_step_td", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(cvrp_step_td)),
      METH_FASTCALL, "CVRPEnv.decode_and_step on a dict-backed TensorDict, in one call"},
+    {"set_inplace", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(set_inplace)),
+     METH_FASTCALL, "allow / forbid the in-place state writes; returns the previous flag"},
+    {"inplace_policy",
+     reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(inplace_policy)),
+     METH_FASTCALL, "(build allows in-place writes, enabled)"},
     {"clear_pool", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(clear_pool)),
      METH_FASTCALL, "drop the pooled step-state storages"},
     {"slab_fresh", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(slab_fresh)),
@@ -1073,5 +1123,7 @@ PyMODINIT_FUNC PyInit__co_torchstep(void) {
   g_attr_i = PyUnicode_InternFromString("_co_i");
   g_attr_tc = PyUnicode_InternFromString("_co_tc");
   if (!g_attr_i || !g_attr_tc) return nullptr;
+  const char* no_inplace = std::getenv("CO_NO_INPLACE");
+  if (no_inplace && no_inplace[0] && no_inplace[0] != '0') g_inplace = false;
   return PyModule_Create(&module);
 }

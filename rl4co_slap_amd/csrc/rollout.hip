@@ -357,6 +357,7 @@ __global__ __launch_bounds__(64 * Q) void tsp_teacher_kernel(
 #ifndef CO_ROWS_DMA
 #define CO_ROWS_DMA 1  // the row kernel stages a wave's rows by LDS-DMA when it can
 #endif
+
 // LDS bytes per wave of the LDS-DMA variant: the wave's GPW coordinate rows and action
 // rows, contiguous in memory, land in LDS as two blocks of GPW*N*8 bytes.
 __host__ __device__ inline size_t tsp_rows_wave_bytes(int gpw, int N) {
@@ -366,8 +367,21 @@ __host__ __device__ inline size_t tsp_rows_wave_bytes(int gpw, int N) {
 // MODE 0: scalar 8-byte action loads; 1: 16-byte vectors (16-byte aligned rows); 2: the
 // wave's GPW action and coordinate rows (contiguous: sb == N, consecutive coordinate
 // rows) staged by LDS-DMA as two contiguous blocks, steps and gathers then read from LDS.
+#ifndef CO_ROWS_WPB
+#define CO_ROWS_WPB 4  // waves per workgroup of the row kernel (r06: 2 / 8 / 16 slower)
+#endif
+// Round 6: the inputs are read once and the outputs written once, so the row kernel's
+// LDS-DMA loads carry the non-temporal hint (nt: streamed past the caches' normal
+// retention) and its mask rows are non-temporal stores -- 23.0 -> 20.7 us per launch at
+// B = 65,536 (HIP events, same box A/B; sc0 / sc1 variants measured no better).
+#ifndef CO_ROWS_AUX
+#define CO_ROWS_AUX 2  // cache-policy bits of the row kernel's LDS-DMA loads (2 = nt)
+#endif
+#ifndef CO_ROWS_NTST
+#define CO_ROWS_NTST 1  // non-temporal mask-row stores
+#endif
 template <int G, int EPL, int MODE, bool STATE>
-__global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
+__global__ __launch_bounds__(64 * CO_ROWS_WPB) void tsp_teacher_rows_kernel(
     int64_t B, int N, const float2* __restrict__ locs, int64_t LB,
     const int64_t* __restrict__ acts, int64_t sb, uint8_t* __restrict__ mask_out,
     int64_t* __restrict__ first_out, int64_t* __restrict__ cur_out, int64_t* __restrict__ i_out,
@@ -377,7 +391,7 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
   // 16-byte action pairs only when every lane's first step t0 = sl*EPL is even (the row
   // base is 16-byte aligned): an odd EPL takes the scalar loads
   constexpr bool VEC = MODE == 1 && EPL % 2 == 0, DMA = MODE == 2;
-  __shared__ uint32_t s_bits[4][GPW][(G * EPL + 31) / 32];
+  __shared__ uint32_t s_bits[CO_ROWS_WPB][GPW][(G * EPL + 31) / 32];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_rows[];  // DMA: per wave
   constexpr int NWB = (G * EPL + 31) / 32;
   const int lane = lane_id(), sl = lane % G, grp = lane / G, w = wave_in_block();
@@ -402,9 +416,10 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
       const int rows = (int)(B - base < GPW ? B - base : GPW);
       const int64_t lb = LB == B ? base : base % LB;
-      wave_dma(reinterpret_cast<const unsigned char*>(locs + lb * N), rows * N * 8, s_w);
-      wave_dma(reinterpret_cast<const unsigned char*>(acts + base * (int64_t)N), rows * N * 8,
-               s_w + half);
+      wave_dma<CO_ROWS_AUX>(reinterpret_cast<const unsigned char*>(locs + lb * N), rows * N * 8,
+                            s_w);
+      wave_dma<CO_ROWS_AUX>(reinterpret_cast<const unsigned char*>(acts + base * (int64_t)N),
+                            rows * N * 8, s_w + half);
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -515,7 +530,10 @@ __global__ __launch_bounds__(256) void tsp_teacher_rows_kernel(
             const uint32_t nib = ~(bits[c4 >> 3] >> (4 * (c4 & 7))) & 0xfu;
             v = (nib & 1u) | ((nib & 2u) << 7) | ((nib & 4u) << 14) | ((nib & 8u) << 21);
           }
-          *reinterpret_cast<uint32_t*>(mrow + 4 * c4) = v;
+          if (CO_ROWS_NTST)
+            __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(mrow + 4 * c4));
+          else
+            *reinterpret_cast<uint32_t*>(mrow + 4 * c4) = v;
         }
       } else {
         for (int c = sl; c < N; c += G)
@@ -644,6 +662,10 @@ __host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O
 #define CO_SLAP_ATTR
 #endif
 
+#ifndef CO_SLAP_NT
+#define CO_SLAP_NT 1  // streaming (non-temporal) loads and stores in the fused SLAP episode
+#endif
+
 template <int G, int EPL, bool CLOSEST>
 __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     int64_t B, int L, int P, int O, int K, const float2* __restrict__ locs,
@@ -654,6 +676,7 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     uint8_t* __restrict__ step_reward_out, float* __restrict__ reward_out,
     float* __restrict__ ratio_out, int32_t* status) {
   constexpr int IPB = 256 / G, GPW = 64 / G;
+  constexpr bool NT = CO_SLAP_NT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // [IPB][P] assignment rows, then one region per wave that holds the sorted candidate
   // keys [EPL][64] during the step loop and, after it (same wave, program order), the
@@ -682,12 +705,12 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     const int c = sl + G * k;
     const bool ok = c < L && c != 0;  // the depot is never free (slap/env.py:115-116)
     if (ok) avail |= 1u << k;
-    dd[k] = (CLOSEST && ok) ? depot_dist[bb * L + c] : __builtin_inff();
+    dd[k] = (CLOSEST && ok) ? ld_s<NT>(depot_dist + bb * L + c) : __builtin_inff();
   }
   // ratio (slap/env.py:114, zeros) depends on nothing: its stores go out first and
   // drain while the loads are in flight
   if (live && ratio_out)
-    for (int c = sl; c < L; c += G) ratio_out[bb * L + c] = 0.f;
+    for (int c = sl; c < L; c += G) st_s<NT>(ratio_out + bb * L + c, 0.f);
   const float2* lrow = locs + bb * L;
   const int64_t* prow = picklist + bb * (int64_t)O * K;
   float2 xr[EPL];
@@ -696,10 +719,10 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
   for (int k = 0; k < EPL; ++k) {
     const int c = sl + G * k;
 #if !CO_SLAP_LATE
-    xr[k] = c < L ? lrow[c] : make_float2(0.f, 0.f);
+    xr[k] = c < L ? ld_s<NT>(lrow + c) : make_float2(0.f, 0.f);
 #endif
 #if CO_SLAP_LATE < 2
-    pr[k] = c < O * K ? prow[c] : 0;
+    pr[k] = c < O * K ? ld_s<NT>(prow + c) : 0;
 #endif
   }
   // closest-free = the free locations in increasing (distance, index) order.  Each lane
@@ -849,7 +872,7 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     const int c = sl + G * k;
     if (c < O * K) pks[c] = (int16_t)pw[k];
   }
-  for (int c = sl + G * EPL; c < O * K; c += G) pks[c] = (int16_t)wrap_product(prow[c]);
+  for (int c = sl + G * EPL; c < O * K; c += G) pks[c] = (int16_t)wrap_product(ld_s<NT>(prow + c));
   // the group's LDS rows are written and read by lanes of the same wave: a wave-level
   // fence orders them, no workgroup barrier (groups do not wait for other waves)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -865,7 +888,7 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     for (int idx = lane; idx < IPW * P; idx += 64) {
       const int t = idx / IPW, gi = idx - t * IPW;
       const int64_t be = (int64_t)blockIdx.x * IPB + w0 + gi;
-      if (be < B) acts_out[(int64_t)t * B + be] = s_asg[(w0 + gi) * P + t];
+      if (be < B) st_s<NT>(acts_out + (int64_t)t * B + be, (int64_t)s_asg[(w0 + gi) * P + t]);
     }
   }
   // one lane per order; for K <= 8 the K picks' LDS lookups (product -> location ->
@@ -905,11 +928,11 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
       const int c = sl + G * k;
-      if (c < L) mrow[c] = (avail >> k) & 1u;
+      if (c < L) st_s<NT>(mrow + c, (uint8_t)((avail >> k) & 1u));
     }
     // (not unrolled: the compiler's 16-way unroll of this loop set the kernel's VGPR peak)
 #pragma unroll 2
-    for (int c = sl; c < P; c += G) assign_out[bb * P + c] = asg[c];
+    for (int c = sl; c < P; c += G) st_s<NT>(assign_out + bb * P + c, asg[c]);
     if (sl == 0) {
       // f32 order-by-order accumulation of slap/env.py:135-142
       float total = 0.f;
@@ -970,11 +993,12 @@ int launch_tsp_rows(int64_t B, int64_t N, const float2* l2, int64_t LB, const in
                       ((reinterpret_cast<uintptr_t>(acts) | reinterpret_cast<uintptr_t>(l2)) & 15) == 0;
 #define CO_ROWS(GG, EE)                                                                        \
   do {                                                                                         \
-    const dim3 grid(cover_grid((B + 64 / GG - 1) / (64 / GG), 4)), block(256);                 \
+    constexpr int WPB = CO_ROWS_WPB;                                                           \
+    const dim3 grid(cover_grid((B + 64 / GG - 1) / (64 / GG), WPB, 64 * WPB)), block(64 * WPB); \
     if (grid.x == 0) return CO_E_INVAL;                                                        \
-    const size_t dsh = 4 * tsp_rows_wave_bytes(64 / GG, (int)N);                               \
+    const size_t dsh = WPB * tsp_rows_wave_bytes(64 / GG, (int)N);                             \
     /* the static visited bitmaps come on top of the dynamic staging (64 KiB default) */       \
-    const size_t sbits = (size_t)4 * (64 / GG) * ((GG * EE + 31) / 32) * 4;                    \
+    const size_t sbits = (size_t)WPB * (64 / GG) * ((GG * EE + 31) / 32) * 4;                  \
     if (dma_ok && (LB == B || LB % (64 / GG) == 0) && dsh + sbits <= 64 * 1024)                \
       hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 2, STATE>), grid, block, dsh, s, B,   \
                          (int)N, l2, LB, acts, sb, mask_out, first_out, cur_out, i_out,        \

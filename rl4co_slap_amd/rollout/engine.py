@@ -292,6 +292,10 @@ class CVRPFusedEpisode(_GraphEpisode):
     [B,N]`` already divided by the capacity); ``vehicle_capacity`` is the env's
     (``cvrp/env.py:126``, ``generator.vehicle_capacity``)."""
 
+    # co_cvrp_rollout packs the step count into 15 bits; an episode ends within 2N + 1 <=
+    # 2,047 steps (N <= 1023), so a larger caller limit is the same limit
+    KERNEL_MAX_STEPS = 0x7fff
+
     def __init__(self, td, vehicle_capacity: float = 1.0, max_steps: int = None,
                  write_locs: bool = True):
         locs = td["locs"]
@@ -325,7 +329,8 @@ class CVRPFusedEpisode(_GraphEpisode):
 
         self._bound = nat.bind(
             "co_cvrp_rollout", self.b, self.n, nat.ptr(self.depot), nat.ptr(self.locs_in),
-            nat.ptr(self.demand), self.vcap, self.max_steps, nat.ptr(self.acts),
+            nat.ptr(self.demand), self.vcap, min(self.max_steps, self.KERNEL_MAX_STEPS),
+            nat.ptr(self.acts),
             nat.ptr(self.locs), nat.ptr(self.cur), nat.ptr(self.used), nat.ptr(self.vcap_t),
             nat.ptr(self.visited), nat.ptr(self.mask), nat.ptr(self.done),
             nat.ptr(self.step_reward), nat.ptr(self.reward), nat.ptr(self.lens),

@@ -14,7 +14,7 @@ C="SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST
 for K in ${PMC_KERNELS:-tsp_stepwise cvrp_stepwise_pair slap_stepwise_closest pomo_tsp100 slap_fused_closest_b65536}; do
   for P in A B C; do
     eval CTRS=\$$P
-    timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d gpurun_out/pmcsq/$K.$P -o run -- python3 tools/pmc_target.py --kernel $K --k 3 > gpurun_out/pmcsq/$K.$P.log 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc $CTRS --output-format csv -d gpurun_out/pmcsq/$K.$P -o run -- python3 tools/pmc_target.py --kernel $K --k 3 ${PMC_ARGS} > gpurun_out/pmcsq/$K.$P.log 2>&1
     rc=$?; echo "[$rc] $K $P"; if [ $rc -ne 0 ]; then tail -3 gpurun_out/pmcsq/$K.$P.log; exit $rc; fi
   done
 done

@@ -198,3 +198,37 @@ def test_slab_reused_only_when_unreferenced(dev):
     td3 = env.reset(TensorDict(dict(data.items()), [b]))
     out3 = pol(td3, env, phase="test", decode_type="greedy", return_actions=True)
     assert torch.equal(out3["actions"], out1["actions"])
+
+
+def test_slab_not_rewritten_across_streams(dev):
+    """an episode start rewrites the step glue's slab from the top only on the
+    stream its rows were handed out on (kernels reading the last episode's rows were queued
+    there); on another stream it takes a new storage, as the state pool does.  Same results
+    either way."""
+    b = 32
+    data = _slap_data(b, dev, 21)
+    logits = torch.randn(b, 100, generator=torch.Generator().manual_seed(8)).to(dev)
+    env = SLAPEnv(device=dev)
+    pol = ConstructivePolicy(None, LogitsDecoder(lambda t: logits), env_name="slap")
+    sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def episode(stream):
+        with torch.cuda.stream(stream):
+            td = env.reset(TensorDict(dict(data.items()), [b]))
+            out = pol(td, env, phase="test", decode_type="greedy", return_actions=True)
+            a = td["action"]  # a slab row: the slab's base address without a storage object
+            ptr = a.data_ptr() - a.storage_offset() * a.element_size()
+            del a
+            acts = out["actions"].clone()
+        stream.synchronize()
+        return ptr, acts
+
+    p1, a1 = episode(sa)
+    p2, a2 = episode(sa)  # same stream, nothing left referring to the slab: reused
+    assert p2 == p1
+    p3, a3 = episode(sb)  # another stream: a new storage
+    assert p3 != p2
+    p4, a4 = episode(sb)
+    assert p4 == p3
+    for a in (a2, a3, a4):
+        assert torch.equal(a, a1)

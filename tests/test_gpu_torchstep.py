@@ -156,3 +156,63 @@ def test_stale_records_fall_back(dev, python_path):
         ref = run()
     _same(glue, ref)
     assert glue["actions"].shape == (b, n)
+
+
+def test_inplace_state_writes_off_gives_same_results(dev):
+    """the SLAP step's in-place assignment / state-block writes rest on
+    CPython reference counts; with them turned off (what a free-threaded or 3.12+ build
+    compiles to, or CO_NO_INPLACE=1) every step takes fresh storages, with the same results."""
+    import numpy as np
+
+    from rl4co_slap_amd.envs import SLAPEnv
+    from rl4co_slap_amd.envs.slap import SLAPGenerator
+
+    ts = nat.torchstep()
+    assert ts is not None
+    b = 64
+    torch.manual_seed(5)
+    np.random.seed(5)
+    data = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
+    logits = torch.randn(b, 100, generator=torch.Generator().manual_seed(9)).to(dev)
+    env = SLAPEnv(device=dev)
+    pol = ConstructivePolicy(None, LogitsDecoder(lambda t: logits), env_name="slap")
+
+    def episode():
+        td = env.reset(TensorDict(dict(data.items()), [b]))
+        out = pol(td, env, phase="test", decode_type="greedy", return_actions=True)
+        return out, td
+
+    from rl4co_slap_amd.utils.decoding import _MODES, math_flags
+
+    mword = _MODES["greedy"] | math_flags("certified")
+    native = env.native_decode_and_step()
+    st = torch.zeros(2, dtype=torch.int32, device=dev)
+
+    def ptrs_over_steps():
+        """storage addresses of the td's assignment / action_mask after steps 1, 2, 3 (the
+        test holds no reference to the tensors themselves)"""
+        td = env.reset(TensorDict(dict(data.items()), [b]))
+        seen = []
+        for k in range(3):
+            out = native(td, logits, mword, 1.0, 0.0, None, 0, k, st, "action")
+            assert out is not None and type(out) is not int
+            del out
+            # data_ptr, not untyped_storage(): a Python storage object can keep a
+            # reference that the glue's use-count test would see
+            seen.append((td["assignment"].data_ptr(), td["action_mask"].data_ptr()))
+        return seen
+
+    on, td_on = episode()
+    seen_on = ptrs_over_steps()
+    assert seen_on[1][0] == seen_on[0][0] and seen_on[2][1] == seen_on[1][1]  # in place
+    prev = ts.set_inplace(False)
+    try:
+        assert ts.inplace_policy()[1] is False
+        seen_off = ptrs_over_steps()
+        assert seen_off[1][0] != seen_off[0][0] and seen_off[2][1] != seen_off[1][1]  # fresh
+        off, td_off = episode()
+    finally:
+        ts.set_inplace(prev)
+    _same(on, off)
+    for k in ("assignment", "action_mask", "i", "done"):
+        assert torch.equal(td_on[k], td_off[k]), k

@@ -152,3 +152,35 @@ def test_fastcall_falls_back_to_ctypes_when_a_library_cannot_load(monkeypatch):
     monkeypatch.setattr(_native, "load", boom)
     assert fc.table("dev") == {}
     assert set(fc.table("host")) == set(_native.HOST_SYMBOLS)
+
+
+def test_step_glue_inplace_guard():
+    """the step glue's in-place state writes (a td-held tensor rewritten
+    when CPython's reference count says nothing else holds it) are compiled in only for the
+    interpreter kind they were tested on (GIL build, < 3.12), can be switched off at run time,
+    and CO_NO_INPLACE=1 forces the fresh-storage fallback from import on."""
+    import subprocess
+    import sys
+    import sysconfig
+
+    ts = _native.torchstep()
+    if ts is None:
+        pytest.skip("step glue not built")
+    build_ok, enabled = ts.inplace_policy()
+    expect = sys.version_info < (3, 12) and not sysconfig.get_config_var("Py_GIL_DISABLED")
+    assert build_ok is expect
+    assert enabled is (expect and not os.environ.get("CO_NO_INPLACE"))
+    prev = ts.set_inplace(False)
+    try:
+        assert ts.inplace_policy() == (build_ok, False)
+        ts.set_inplace(True)
+        assert ts.inplace_policy() == (build_ok, build_ok)  # never on where the build forbids it
+    finally:
+        ts.set_inplace(prev)
+    code = ("from rl4co_slap_amd import _native as nat; p = nat.torchstep().inplace_policy(); "
+            "print(int(p[0]), int(p[1]))")
+    env = dict(os.environ, CO_NO_INPLACE="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         cwd=ROOT, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.split()[-2:] == [str(int(expect)), "0"]

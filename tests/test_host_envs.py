@@ -186,3 +186,23 @@ def test_mixed_devices_and_missing_host_symbols_raise():
         td["action"] = torch.zeros(3, dtype=torch.int64, device="cuda")
         with pytest.raises(RuntimeError, match="mixed devices"):
             env.step(td)
+
+
+@pytest.mark.parametrize("clip", [0.0, 10.0])
+def test_process_logits_does_not_write_the_callers_logits(clip):
+    """VERDICT r5 item 7, a deliberate deviation: with tanh_clipping == 0 and
+    mask_logits the reference's process_logits writes -inf into the caller's logits tensor
+    (decoding.py:178, ``logits[~mask] = -inf`` on its argument).  The fused decode never
+    writes its input; the log-probabilities are the reference's bit for bit."""
+    from rl4co_slap_amd.utils.decoding import process_logits
+
+    g = torch.Generator().manual_seed(17)
+    logits = torch.randn(16, 20, generator=g)
+    mask = torch.rand(16, 20, generator=g) < 0.6
+    mask[:, 3] = True
+    before = logits.clone()
+    full = process_logits(logits, mask, tanh_clipping=clip)
+    assert torch.equal(logits, before)
+    ref_in = logits.clone()
+    want = ref_process_logits(ref_in, mask, 1.0, clip, tanh=tanh_cr)
+    assert torch.equal(full, want)

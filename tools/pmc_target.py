@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 ap = argparse.ArgumentParser()
 ap.add_argument("--kernel", default="tsp_fused_teacher")
 ap.add_argument("--k", type=int, default=5)
+ap.add_argument("--cycle", type=int, default=1,
+                help="distinct input batches run in turn (4: the fused modes read HBM, not MALL)")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 from rl4co_slap_amd import _native  # noqa: E402
@@ -63,6 +65,10 @@ elif args.kernel.startswith("tsp"):
     acts = torch.rand(65536, 100).argsort(1)
     if args.kernel == "tsp_fused_teacher":
         ep = engine.TSPFusedEpisode(locs.to(dev), acts.to(dev))
+        if args.cycle > 1:
+            eps = [ep] + [engine.TSPFusedEpisode(torch.rand(65536, 100, 2, device=dev),
+                                                 torch.rand(65536, 100, device=dev).argsort(1))
+                          for _ in range(args.cycle - 1)]
     elif args.kernel == "tsp_fused_nearest":
         ep = engine.TSPFusedEpisode(locs.to(dev), None, policy="nearest")
     else:
@@ -109,7 +115,13 @@ else:
         ep = engine.SLAPFusedEpisode(td, acts, policy="teacher")
     else:
         ep = engine.SLAPFusedEpisode(td, None, policy="closest")
-for _ in range(args.k):
-    ep.run_eager()
+        if args.cycle > 1:
+            eps = [ep] + [engine.SLAPFusedEpisode(SLAPGenerator(materialize_dist_mat=False)(b).to(dev),
+                                                  None, policy="closest")
+                          for _ in range(args.cycle - 1)]
+if "eps" not in globals():
+    eps = [ep]
+for j in range(args.k * len(eps)):
+    eps[j % len(eps)].run_eager()
 torch.cuda.synchronize()
 print("ok", args.kernel)
