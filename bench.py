@@ -577,6 +577,29 @@ def main():
         "achieved_GBps": b * n * sw_bytes * k / ev_s / 1e9,
         "frac": b * n * sw_bytes * k / ev_s / 1e9 / HBM_PEAK_GBS,
         "frac_wall": b * n * sw_bytes * k / wall_s / 1e9 / HBM_PEAK_GBS}
+    # ---- the same per-step loop with the steps in chunks of 10 per launch (co_tsp_steps,
+    # round 6): every step's state is still written to HBM (the ping-pong buffers, as the
+    # one-launch-per-step loop writes them; bit-identical), the state is carried in
+    # registers inside a chunk instead of re-read.  Bytes it moves per env-step: the mask
+    # row N + action 8 + i / first / current 24 + done / reward 2, the chunk's state read
+    # (N + 16) / 10, the reward's (16N + 4) / N -- not the one-launch contract's 2N + 50.
+    kc = 10
+    swc = TSPStepwiseEpisode(locs, acts, policy="teacher", check=True, chunk=kc).capture()
+    wall_c, ev_c = timed(swc.replay, k, 2, world, dev)
+    assert int(swc.status.item()) == 0, "TSP chunked stepwise episode status"
+    del swc
+    t_c = max_over_ranks(wall_c, world, dev)
+    swc_bytes = n + 34 + (n + 16) / kc + (16 * n + 4) / n
+    out["tsp_stepwise_chunked"] = {
+        "value": world * b * n * k / t_c, "unit": "env-steps/s", "ms_per_episode": t_c / k * 1e3,
+        "workload": f"TSP-{n} B={b}/GPU teacher-forced episode, {kc} env steps per co_tsp_steps "
+                    "launch (every step's state written to HBM), reset + reward included, HIP "
+                    "graph",
+        "steps_per_launch": kc, "alg_bytes_per_env_step": swc_bytes,
+        "contract_bytes_per_env_step_one_launch_loop": sw_bytes,
+        "achieved_GBps": b * n * swc_bytes * k / ev_c / 1e9,
+        "frac": b * n * swc_bytes * k / ev_c / 1e9 / HBM_PEAK_GBS,
+        "frac_wall": b * n * swc_bytes * k / wall_c / 1e9 / HBM_PEAK_GBS}
     # ---- SLAP at the north star's batch (B = 65,536; examples/slap.py instance)
     slap65 = bench_slap(65536, k, world, rank, dev)
     fc, sc = slap65["slap_fused_closest"], slap65["slap_stepwise_graph"]
@@ -658,7 +681,7 @@ def main():
         order = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
                  "roofline", "cpu_baseline"]
-        last = ["tsp_stepwise", "slap_b65536", "summary"]
+        last = ["tsp_stepwise", "tsp_stepwise_chunked", "slap_b65536", "summary"]
         final = {key: out[key] for key in order if key in out}
         final.update({key: v for key, v in out.items() if key not in final and key not in last})
         final.update({key: out[key] for key in last if key in out})
@@ -698,6 +721,11 @@ def summarize(out):
         t = out["tsp_stepwise"]
         sm["tsp100_stepwise"] = {"env_steps_s": r(t["value"], 0), "frac": r(t["frac"]),
                                  "frac_wall": r(t["frac_wall"])}
+    if "tsp_stepwise_chunked" in out:
+        t = out["tsp_stepwise_chunked"]
+        sm["tsp100_stepwise_chunked"] = {"env_steps_s": r(t["value"], 0), "frac": r(t["frac"]),
+                                         "frac_wall": r(t["frac_wall"]),
+                                         "steps_per_launch": t["steps_per_launch"]}
     if "slap_b65536" in out:
         t = out["slap_b65536"]
         sm["slap_b65536_fused"] = {"env_steps_s": r(t["value"], 0),

@@ -70,6 +70,20 @@ int co_tsp_step(int64_t batch, int64_t num_loc, const int64_t* action, const uin
                 int64_t* first_out, int64_t* current_out, uint8_t* done, uint8_t* reward,
                 int first_mode, const int32_t* first_flag, int32_t* status, void* stream);
 
+/* K consecutive TSPEnv._step calls (tsp/env.py:67-93) in one launch (round 6): exactly the
+ * K co_tsp_step launches t = 0..K-1 with action row t at action + t*act_stride and the
+ * state ping-ponging between buffers A and B (step t reads A and writes B for even t, the
+ * reverse for odd t; current_out / done / reward written by every step), so every step's
+ * state is stored as its own launch would store it and the final contents are
+ * bit-identical.  first_mode (step 0 only): 0 = keep first_a, 1 = take action (the
+ * episode's first step).  Rows the lane-group kernel does not take (N % 4 != 0, tiny N)
+ * run as the K single-step launches.  Replaces K env.step() calls of a loop whose actions
+ * are known in advance (teacher forcing, the stepwise engine). */
+int co_tsp_steps(int64_t batch, int64_t num_loc, int64_t steps, const int64_t* action,
+                 int64_t act_stride, uint8_t* mask_a, int64_t* i_a, int64_t* first_a,
+                 uint8_t* mask_b, int64_t* i_b, int64_t* first_b, int64_t* current_out,
+                 uint8_t* done, uint8_t* reward, int first_mode, int32_t* status, void* stream);
+
 /* TSPEnv.get_reward (envs/common/base.py:182-188 + tsp/env.py:157-173):
  * reward[b] = -closed tour length of locs[b % locs_batch, actions[b, 0..T-1]]
  * (locs_batch = batch normally; = instances for the POMO [S, B] multistart layout,

@@ -285,6 +285,10 @@ typedef __attribute__((address_space(3))) void lds_void;
 // round trip, all pieces in flight before the single wait.  `src` and `dst` must be
 // 16-byte aligned; a tail of < 16 bytes is copied with plain loads.  Ends with the
 // vmcnt drain + workgroup barrier that make the tile visible.
+#ifndef CO_STAGE_AUX
+#define CO_STAGE_AUX 0  // cache-policy bits of stage_bytes_lds's LDS-DMA (2 = nt)
+#endif
+template <int AUX = CO_STAGE_AUX>
 __device__ __forceinline__ void stage_bytes_lds(const unsigned char* __restrict__ src, int nbytes,
                                                 unsigned char* dst) {
   const int lane = threadIdx.x & 63, wave = wave_in_block(), nw = blockDim.x >> 6;
@@ -292,7 +296,8 @@ __device__ __forceinline__ void stage_bytes_lds(const unsigned char* __restrict_
   for (int base = wave * 1024; base < n16; base += nw * 1024) {
     const int off = base + lane * 16;
     if (off < n16)
-      __builtin_amdgcn_global_load_lds((const void*)(src + off), (lds_void*)(dst + base), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(src + off), (lds_void*)(dst + base), 16, 0,
+                                       AUX);
   }
   for (int k = n16 + (int)threadIdx.x; k < nbytes; k += blockDim.x) dst[k] = src[k];
   __builtin_amdgcn_s_waitcnt(0);

@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(64 * Q) void cvrp_reward_tile_kernel(
     for (int base = (q - 1) * 1024; q > 0 && base < d16; base += (Q - 1) * 1024)
       if (base + lane * 16 < d16)
         __builtin_amdgcn_global_load_lds((const void*)(dsrc + base + lane * 16),
-                                         (lds_void*)(smem + L.dem + base), 16, 0, 0);
+                                         (lds_void*)(smem + L.dem + base), 16, 0, CO_STAGE_AUX);
     for (int k = d16 + (int)threadIdx.x; k < dbytes; k += 64 * Q) smem[L.dem + k] = dsrc[k];
   }
   stage_bytes_lds(reinterpret_cast<const unsigned char*>(locs + row0 * NC), rows * NC * 8,

@@ -31,16 +31,19 @@ namespace {
 // an explicit drain + wave barrier.
 // Whole 64-lane pieces carry no per-lane predicate (a branch per DMA instruction cost more
 // VALU / SALU than the copy itself); only the tail piece masks lanes.
+#ifndef CO_ENVSTAGE_AUX
+#define CO_ENVSTAGE_AUX 0  // cache-policy bits of the env staging DMA (2 = nt)
+#endif
 template <class F>
 __device__ __forceinline__ void dma_dwords(int n, uint32_t* lds_dst, F src) {
   const int lane = lane_id();
   int base = 0;
   for (; base + 64 <= n; base += 64)  // wave-uniform trip count
     __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + base), 4,
-                                     0, 0);
+                                     0, CO_ENVSTAGE_AUX);
   if (base < n && lane < n - base)
     __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + base), 4,
-                                     0, 0);
+                                     0, CO_ENVSTAGE_AUX);
 }
 
 // n4 16-byte units (src(k): the k-th, 16-byte aligned) to a 16-byte aligned LDS destination:
@@ -51,10 +54,10 @@ __device__ __forceinline__ void dma_dwordx4(int n4, uint32_t* lds_dst, F src) {
   int base = 0;
   for (; base + 64 <= n4; base += 64)
     __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + 4 * base),
-                                     16, 0, 0);
+                                     16, 0, CO_ENVSTAGE_AUX);
   if (base < n4 && lane < n4 - base)
     __builtin_amdgcn_global_load_lds((const void*)src(base + lane), (lds_void*)(lds_dst + 4 * base),
-                                     16, 0, 0);
+                                     16, 0, CO_ENVSTAGE_AUX);
 }
 
 __device__ __forceinline__ void stage_ready() {

@@ -600,18 +600,14 @@ __device__ __forceinline__ float edge_len_hw(float x0, float y0, float x1, float
   return __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
 }
 __device__ __forceinline__ int slap_pick_loc(int pp, const int32_t* asg, int L, bool& range) {
-  int64_t loc = 0;
-  if (pp < 0) {
-    range = true;
-  } else {
-    loc = asg[pp];
-    if (loc < 0) loc += L;
-    if (loc < 0 || loc >= L) {
-      range = true;
-      loc = 0;
-    }
-  }
-  return (int)loc;
+  // branch-free (r06): the assignment entry is read at a clamped index and every test is
+  // a select; the wave runs one straight-line path per pick
+  const bool neg = pp < 0;
+  int64_t loc = asg[neg ? 0 : pp];
+  loc = loc < 0 ? loc + L : loc;
+  const bool bad = neg || loc < 0 || loc >= L;
+  range |= bad;
+  return bad ? 0 : (int)loc;
 }
 template <int KU, typename PK>
 __device__ __forceinline__ float slap_order_len(const PK* pk, const int32_t* asg,
@@ -663,7 +659,8 @@ __host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O
 #endif
 
 #ifndef CO_SLAP_NT
-#define CO_SLAP_NT 1  // streaming (non-temporal) loads and stores in the fused SLAP episode
+#define CO_SLAP_NT 0  // non-temporal loads / stores (r06: 47 -> 53 us at B = 65,536: partial-line
+                      // accesses; nt pays only for whole-line streams such as LDS-DMA)
 #endif
 
 template <int G, int EPL, bool CLOSEST>
@@ -709,8 +706,16 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
   }
   // ratio (slap/env.py:114, zeros) depends on nothing: its stores go out first and
   // drain while the loads are in flight
-  if (live && ratio_out)
-    for (int c = sl; c < L; c += G) st_s<NT>(ratio_out + bb * L + c, 0.f);
+  if (live && ratio_out) {
+    float* rrow = ratio_out + bb * L;
+    if (((reinterpret_cast<uintptr_t>(ratio_out) | ((uintptr_t)L * 4)) & 15) == 0) {
+      // 16-byte stores (r06): 2 store instructions per lane at L = 100 instead of 7
+      for (int c4 = sl; c4 < (L >> 2); c4 += G)
+        *reinterpret_cast<float4*>(rrow + 4 * c4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      for (int c = sl; c < L; c += G) st_s<NT>(rrow + c, 0.f);
+    }
+  }
   const float2* lrow = locs + bb * L;
   const int64_t* prow = picklist + bb * (int64_t)O * K;
   float2 xr[EPL];
@@ -925,18 +930,51 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
 #endif
   if (live) {
     uint8_t* mrow = mask_out + bb * L;
+    if (((reinterpret_cast<uintptr_t>(mask_out) | (uintptr_t)L) & 3) == 0) {
+      // r06: the mask bytes go through the group's coordinate slot in LDS (free after the
+      // reward) and out as dwords -- 2 store instructions per lane at L = 100, not 8 byte
+      // stores
+      uint8_t* sm = reinterpret_cast<uint8_t*>(xy);
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) {
-      const int c = sl + G * k;
-      if (c < L) st_s<NT>(mrow + c, (uint8_t)((avail >> k) & 1u));
+      for (int k = 0; k < EPL; ++k) {
+        const int c = sl + G * k;
+        if (c < L) sm[c] = (uint8_t)((avail >> k) & 1u);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int d = sl; d < (L >> 2); d += G)
+        *reinterpret_cast<uint32_t*>(mrow + 4 * d) = *reinterpret_cast<const uint32_t*>(sm + 4 * d);
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) {
+        const int c = sl + G * k;
+        if (c < L) st_s<NT>(mrow + c, (uint8_t)((avail >> k) & 1u));
+      }
     }
-    // (not unrolled: the compiler's 16-way unroll of this loop set the kernel's VGPR peak)
+    if (((reinterpret_cast<uintptr_t>(assign_out) | ((uintptr_t)P * 4)) & 15) == 0) {
+      for (int c4 = sl; c4 < (P >> 2); c4 += G)  // the row as 16-byte pieces
+        *reinterpret_cast<int4*>(assign_out + bb * P + 4 * c4) =
+            *reinterpret_cast<const int4*>(asg + 4 * c4);
+    } else {
+      // (not unrolled: the compiler's 16-way unroll of this loop set the kernel's VGPR peak)
 #pragma unroll 2
-    for (int c = sl; c < P; c += G) st_s<NT>(assign_out + bb * P + c, asg[c]);
+      for (int c = sl; c < P; c += G) st_s<NT>(assign_out + bb * P + c, asg[c]);
+    }
     if (sl == 0) {
-      // f32 order-by-order accumulation of slap/env.py:135-142
+      // f32 order-by-order accumulation of slap/env.py:135-142 (four lengths per LDS read
+      // when the row allows it: the reads no longer wait one by one)
       float total = 0.f;
-      for (int o = 0; o < O; ++o) total += -olen[o];
+      int o = 0;
+      if ((O & 3) == 0 && (reinterpret_cast<uintptr_t>(olen) & 15) == 0)
+        for (; o < O; o += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(olen + o);
+          total += -v.x;
+          total += -v.y;
+          total += -v.z;
+          total += -v.w;
+        }
+      for (; o < O; ++o) total += -olen[o];
       reward_out[bb] = total;
       i_out[bb] = P;
       done_out[bb] = 1;  // the P-th step has i == P-1

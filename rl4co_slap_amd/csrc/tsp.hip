@@ -190,6 +190,86 @@ __global__ __launch_bounds__(256) void tsp_step_group_kernel(int64_t B, int N,
 #undef CO_TSP_WORD
 }
 
+// K consecutive env steps in one launch (co_tsp_steps, round 6): exactly K co_tsp_step
+// calls whose state ping-pongs between the buffers A and B (step k reads A for even k, B
+// for odd k, and writes the other), every step's mask row, i, first node, current node,
+// done and reward stored as that step's launch would store them.  The row's state is
+// loaded once, then carried in registers from step to step (each step still writes its
+// whole state).  G lanes per row, the group kernel's word layout (word c = sl + k*G,
+// WPL words per lane); the K actions of the row are loaded up front (KB per batch).
+template <int G>
+__global__ __launch_bounds__(256) void tsp_steps_group_kernel(
+    int64_t B, int N, int K, const int64_t* __restrict__ action, int64_t astride,
+    uint32_t* __restrict__ mask_a, int64_t* __restrict__ i_a, int64_t* __restrict__ first_a,
+    uint32_t* __restrict__ mask_b, int64_t* __restrict__ i_b, int64_t* __restrict__ first_b,
+    int64_t* __restrict__ cur_out, uint8_t* __restrict__ done, uint8_t* __restrict__ reward,
+    int first_mode, int32_t* status) {
+  constexpr int WPL = CO_TSP_WPL, KB = 8;
+  const int lane = lane_id(), sl = lane % G, gbase = lane - sl;
+  const int W = N >> 2;
+  const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
+  const uint64_t gmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+  const int64_t b0 = wid * (64 / G);
+  if (b0 >= B) return;  // wave-uniform
+  const int64_t bq = b0 + lane / G;
+  const bool valid = bq < B;
+  const int64_t r = valid ? bq : 0;
+  uint32_t w[WPL];
+#pragma unroll
+  for (int k = 0; k < WPL; ++k) {
+    const int c = sl + k * G;
+    w[k] = (valid && c < W) ? mask_a[r * W + c] : 0u;
+  }
+  int64_t iv = valid ? i_a[r] : 0;
+  int64_t fv = (valid && first_mode != 1) ? first_a[r] : 0;
+  bool range = false;
+  for (int t0 = 0; t0 < K; t0 += KB) {
+    int64_t av[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      av[u] = (valid && t0 + u < K) ? action[(int64_t)(t0 + u) * astride + r] : 0;
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int t = t0 + u;
+      if (t >= K) break;  // wave-uniform
+      const int64_t a_raw = av[u];
+      int64_t a = a_raw;
+      if (a < 0 || a >= N) {
+        range |= valid;
+        a = -1;
+      }
+      const int aw = a >= 0 ? (int)(a >> 2) : -1;
+      const uint32_t aclr = 0xffu << (8 * (int)(a & 3));
+      int left = 0;
+#pragma unroll
+      for (int k = 0; k < WPL; ++k) {
+        const uint32_t clr = sl + k * G == aw ? aclr : 0u;
+        w[k] &= ~clr;
+        const uint32_t nz = (((w[k] & 0x7f7f7f7fu) + 0x7f7f7f7fu) | w[k]) & 0x80808080u;
+        left += __builtin_popcount(nz);
+      }
+      const bool to_b = (t & 1) == 0;  // step t writes B when it read A
+      uint32_t* mdst = (to_b ? mask_b : mask_a) + r * W;
+#pragma unroll
+      for (int k = 0; k < WPL; ++k) {
+        const int c = sl + k * G;
+        if (valid && c < W) mdst[c] = w[k];
+      }
+      const bool any_left = (__ballot(left != 0) & gmask) != 0;
+      iv += 1;
+      if (t == 0 && first_mode == 1) fv = a_raw;
+      if (valid) {
+        if (sl == 0) (to_b ? i_b : i_a)[r] = iv;
+        else if (sl == 1) (to_b ? first_b : first_a)[r] = fv;
+        else if (sl == 2 && cur_out) cur_out[r] = a_raw;
+        else if (sl == 3) done[r] = !any_left;
+        else if (sl == 4 % G) reward[r] = 0;
+      }
+    }
+  }
+  if (__any(range) && lane == 0) set_status(status, CO_ST_INDEX_RANGE);
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void tsp_reward_kernel(int64_t B, int N, int T,
                                                                 const float2* locs, int64_t LB,
@@ -321,6 +401,53 @@ extern "C" int co_tsp_step(int64_t B, int64_t N, const int64_t* action, const ui
   if (grid == 0) return CO_E_INVAL;
   hipLaunchKernelGGL(tsp_step_kernel, dim3(grid), dim3(kTileThreads), 0, (hipStream_t)stream, B,
                      (int)N, action, mask_in, mask_out, epi, first_mode, first_flag, status, vec);
+  return launch_status();
+}
+
+extern "C" int co_tsp_steps(int64_t B, int64_t N, int64_t K, const int64_t* action,
+                            int64_t astride, uint8_t* mask_a, int64_t* i_a, int64_t* first_a,
+                            uint8_t* mask_b, int64_t* i_b, int64_t* first_b,
+                            int64_t* current_out, uint8_t* done, uint8_t* reward,
+                            int first_mode, int32_t* status, void* stream) {
+  if (B < 0 || N <= 0 || N > (1 << 30) || K < 0 || K > (1 << 20)) return CO_E_INVAL;
+  if (B == 0 || K == 0) return CO_OK;
+  if (first_mode < 0 || first_mode > 1) return CO_E_MODE;
+  if (!action || astride < B || !mask_a || !i_a || !mask_b || !i_b || !first_b || !done ||
+      !reward || !status || (first_mode == 0 && !first_a) || (K > 1 && !first_a))
+    return CO_E_INVAL;
+  const int W = (int)(N >> 2), WG = (W + CO_TSP_WPL - 1) / CO_TSP_WPL;
+  const bool group = (N & 3) == 0 && W <= 64 * CO_TSP_WPL && WG >= 5 &&
+                     ((reinterpret_cast<uintptr_t>(mask_a) | reinterpret_cast<uintptr_t>(mask_b)) &
+                      3) == 0;
+  if (!group) {  // the K single steps (rows the group kernel does not take)
+    for (int64_t t = 0; t < K; ++t) {
+      const bool even = (t & 1) == 0;
+      const int rc = co_tsp_step(B, N, action + t * astride, even ? mask_a : mask_b,
+                                 even ? mask_b : mask_a, even ? i_a : i_b, even ? i_b : i_a,
+                                 even ? first_a : first_b, even ? first_b : first_a,
+                                 current_out, done, reward, t == 0 ? first_mode : 0, nullptr,
+                                 status, stream);
+      if (rc != CO_OK) return rc;
+    }
+    return CO_OK;
+  }
+  // G >= 8: the row scalars go out from lanes 0-4 of the group
+  const int G = WG <= 8 ? 8 : WG <= 16 ? 16 : WG <= 32 ? 32 : 64;
+  const int64_t waves = (B * G + 63) / 64;
+  const dim3 grid(cover_grid(waves, 4));
+  if (grid.x == 0) return CO_E_INVAL;
+  uint32_t* ma = reinterpret_cast<uint32_t*>(mask_a);
+  uint32_t* mb = reinterpret_cast<uint32_t*>(mask_b);
+  hipStream_t s = (hipStream_t)stream;
+#define CO_TSK(GG)                                                                             \
+  hipLaunchKernelGGL(tsp_steps_group_kernel<GG>, grid, dim3(256), 0, s, B, (int)N, (int)K,     \
+                     action, astride, ma, i_a, first_a, mb, i_b, first_b, current_out, done,  \
+                     reward, first_mode, status)
+  if (G == 8) CO_TSK(8);
+  else if (G == 16) CO_TSK(16);
+  else if (G == 32) CO_TSK(32);
+  else CO_TSK(64);
+#undef CO_TSK
   return launch_status();
 }
 

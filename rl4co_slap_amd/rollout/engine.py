@@ -57,13 +57,18 @@ class _GraphEpisode:
 
 
 class TSPStepwiseEpisode(_GraphEpisode):
-    """Reset + N x co_tsp_step (+ optional in-kernel nearest policy) + co_tsp_reward."""
+    """Reset + N x co_tsp_step (+ optional in-kernel nearest policy) + co_tsp_reward.
+
+    ``chunk`` > 1 (teacher actions): the steps go out as ceil(N / chunk) co_tsp_steps
+    launches of `chunk` steps each -- the same per-step state writes into the same
+    ping-pong buffers (bit-identical), fewer launch boundaries."""
 
     def __init__(self, locs: torch.Tensor, actions: torch.Tensor = None, policy: str = "teacher",
-                 check: bool = True):
+                 check: bool = True, chunk: int = 1):
         super().__init__(locs.device)
         b, n, _ = locs.shape
         self.b, self.n, self.policy, self.check = b, n, policy, check
+        self.chunk = max(1, int(chunk)) if policy == "teacher" else 1
         d = locs.device
         self.locs = locs.contiguous()
         if policy == "teacher":
@@ -85,7 +90,15 @@ class TSPStepwiseEpisode(_GraphEpisode):
         b, n = self.b, self.n
         nat.call("co_tsp_reset", b, n, nat.ptr(self.mask[0]), nat.ptr(self.first[0]),
                  nat.ptr(self.cur), nat.ptr(self.i[0]), nat.ptr(self.reset_reward), s)
-        for t in range(n):
+        for t0 in range(0, n if self.chunk > 1 else 0, self.chunk):
+            k = min(self.chunk, n - t0)
+            a_, b_ = t0 & 1, (t0 + 1) & 1  # step t0 reads buffer a_ (the ping-pong parity)
+            nat.call("co_tsp_steps", b, n, k, nat.ptr(self.acts[t0]), b, nat.ptr(self.mask[a_]),
+                     nat.ptr(self.i[a_]), nat.ptr(self.first[a_]), nat.ptr(self.mask[b_]),
+                     nat.ptr(self.i[b_]), nat.ptr(self.first[b_]), nat.ptr(self.cur),
+                     nat.ptr(self.done), nat.ptr(self.step_reward), 1 if t0 == 0 else 0,
+                     nat.ptr(self.status), s)
+        for t in range(n if self.chunk == 1 else 0):
             src, dst = t & 1, (t + 1) & 1
             a = self.acts[t]
             if self.policy == "nearest":
