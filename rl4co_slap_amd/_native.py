@@ -108,6 +108,8 @@ def load():
                 "`python -m rl4co_slap_amd.csrc.build` (hipcc, gfx950). There is no CPU fallback.")
         lib = ctypes.CDLL(LIB_PATH)
         for name, argtypes in _SIGS.items():
+            if LIB_PATH != _PRODUCT_LIB_PATH and not hasattr(lib, name):
+                continue  # an older variant library a measurement tool points at
             fn = getattr(lib, name)
             fn.argtypes = argtypes
             fn.restype = ctypes.c_int
