@@ -640,6 +640,20 @@ __host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O
   const size_t data = (size_t)gpw * (L * 8 + O * 4 + O * K * 2);
   return ((keys > data ? keys : data) + 15) & ~(size_t)15;
 }
+// The LDS-DMA staging layout (SD = true): the wave's coordinate rows [GPW][L] land at the
+// region's start by DMA and stay there; after them one area holds, in turn, the DMA'd depot
+// distances [GPW][L], the sorted keys 2..EPL-1 [EPL-2][64], and after the step loop the
+// order lengths [GPW][O] and picklist products [GPW][O*K].
+__host__ __device__ inline size_t slap_xy_bytes(int gpw, int L) {
+  return ((size_t)gpw * L * 8 + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t slap_wave_bytes_sd(int gpw, int epl, int L, int O, int K) {
+  size_t area = (size_t)(epl - 2) * 64 * 8;
+  const size_t dd = (size_t)gpw * L * 4, tail = (size_t)gpw * (O * 4 + O * K * 2);
+  area = area > dd ? area : dd;
+  area = area > tail ? area : tail;
+  return slap_xy_bytes(gpw, L) + ((area + 15) & ~(size_t)15);
+}
 
 #ifndef CO_SLAP_LATE
 #define CO_SLAP_LATE 0  // 1: the coordinates, 2: also the picklist loaded after the step loop
@@ -663,7 +677,15 @@ __host__ __device__ inline size_t slap_wave_bytes(int gpw, int epl, int L, int O
                       // accesses; nt pays only for whole-line streams such as LDS-DMA)
 #endif
 
-template <int G, int EPL, bool CLOSEST>
+#ifndef CO_SLAP_SD
+#define CO_SLAP_SD 1  // stage coordinates and depot distances by LDS-DMA (nt) when aligned
+                      // (r06: B = 16,384 18.9 -> 17.0 us, 65,536 48.0 -> 45.1 us, A/B)
+#endif
+#ifndef CO_SLAP_PNT
+#define CO_SLAP_PNT 0  // picklist loads non-temporal (r06: 44.8 -> 47.2 us at B = 65,536: off)
+#endif
+
+template <int G, int EPL, bool CLOSEST, bool SD>
 __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     int64_t B, int L, int P, int O, int K, const float2* __restrict__ locs,
     const int64_t* __restrict__ picklist, const float* __restrict__ depot_dist,
@@ -680,16 +702,36 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
   // coordinates [GPW][L], order lengths [GPW][O] and picklist products [GPW][O*K]
   const int lane = lane_id(), sl = lane % G, g = threadIdx.x / G, gw = lane / G;
   int32_t* s_asg = reinterpret_cast<int32_t*>(smem);
-  unsigned char* wreg = smem + slap_asg_bytes(IPB, P) +
-                        (size_t)wave_in_block() * slap_wave_bytes(GPW, EPL, L, O, K);
-  uint64_t* s_keys = reinterpret_cast<uint64_t*>(wreg);
+  unsigned char* wreg =
+      smem + slap_asg_bytes(IPB, P) +
+      (size_t)wave_in_block() * (SD ? slap_wave_bytes_sd(GPW, EPL, L, O, K)
+                                    : slap_wave_bytes(GPW, EPL, L, O, K));
+  // SD: keys 2..EPL-1 at slots 0..EPL-3 of the area after the coordinates; else slots
+  // 2..EPL-1 of the region's start (overwritten by the coordinates after the loop)
+  unsigned char* area = wreg + (SD ? slap_xy_bytes(GPW, L) : 0);
+  uint64_t* s_keys = reinterpret_cast<uint64_t*>(area) - (SD ? 2 * 64 : 0);
   const int64_t b = (int64_t)blockIdx.x * IPB + g;
   const bool live = b < B;
   const int64_t bb = live ? b : 0;
   float2* xy = reinterpret_cast<float2*>(wreg) + gw * L;
   int32_t* asg = s_asg + g * P;
-  float* olen = reinterpret_cast<float*>(wreg + (size_t)GPW * L * 8) + gw * O;
-  int16_t* pks = reinterpret_cast<int16_t*>(wreg + (size_t)GPW * (L * 8 + O * 4)) + gw * O * K;
+  unsigned char* obase = SD ? area : wreg + (size_t)GPW * L * 8;
+  float* olen = reinterpret_cast<float*>(obase) + gw * O;
+  int16_t* pks = reinterpret_cast<int16_t*>(obase + (size_t)GPW * O * 4) + gw * O * K;
+  // SD: the wave's GPW depot-distance rows and coordinate rows (contiguous in memory) by
+  // LDS-DMA with the non-temporal hint, the distances first: the wait for them (the sort
+  // needs them) is the only one before the step loop; the coordinates are waited for after
+  // it
+  const int64_t wbase = (int64_t)blockIdx.x * IPB + (int64_t)wave_in_block() * GPW;
+  const int wrows = (int)(B - wbase < GPW ? (B - wbase > 0 ? B - wbase : 0) : GPW);
+  if constexpr (SD) {
+    wave_dma<2>(reinterpret_cast<const unsigned char*>(depot_dist + wbase * L), wrows * L * 4,
+                area);
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
 
   // Loads are issued in the order they are needed: the depot distances (the step loop),
   // then the coordinates and up to G*EPL picklist entries, which stay in registers during
@@ -702,7 +744,14 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     const int c = sl + G * k;
     const bool ok = c < L && c != 0;  // the depot is never free (slap/env.py:115-116)
     if (ok) avail |= 1u << k;
-    dd[k] = (CLOSEST && ok) ? ld_s<NT>(depot_dist + bb * L + c) : __builtin_inff();
+    if constexpr (SD)
+      dd[k] = (CLOSEST && ok) ? reinterpret_cast<const float*>(area)[gw * L + c] : __builtin_inff();
+    else
+      dd[k] = (CLOSEST && ok) ? ld_s<NT>(depot_dist + bb * L + c) : __builtin_inff();
+  }
+  if constexpr (SD) {  // the coordinates stream in behind the sort and the step loop
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the distance reads are back
+    wave_dma<2>(reinterpret_cast<const unsigned char*>(locs + wbase * L), wrows * L * 8, wreg);
   }
   // ratio (slap/env.py:114, zeros) depends on nothing: its stores go out first and
   // drain while the loads are in flight
@@ -724,10 +773,10 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
   for (int k = 0; k < EPL; ++k) {
     const int c = sl + G * k;
 #if !CO_SLAP_LATE
-    xr[k] = c < L ? ld_s<NT>(lrow + c) : make_float2(0.f, 0.f);
+    if constexpr (!SD) xr[k] = c < L ? ld_s<NT>(lrow + c) : make_float2(0.f, 0.f);
 #endif
 #if CO_SLAP_LATE < 2
-    pr[k] = c < O * K ? ld_s<NT>(prow + c) : 0;
+    pr[k] = c < O * K ? ld_s<NT || CO_SLAP_PNT>(prow + c) : 0;
 #endif
   }
   // closest-free = the free locations in increasing (distance, index) order.  Each lane
@@ -856,13 +905,17 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
     return;
   }
 #endif
+  if constexpr (SD) {  // the DMA'd coordinates have landed in place
+    __builtin_amdgcn_s_waitcnt(0);
+  } else {
 #pragma unroll
-  for (int k = 0; k < EPL; ++k) {
-    const int c = sl + G * k;
+    for (int k = 0; k < EPL; ++k) {
+      const int c = sl + G * k;
 #if CO_SLAP_LATE
-    xr[k] = c < L ? lrow[c] : make_float2(0.f, 0.f);
+      xr[k] = c < L ? lrow[c] : make_float2(0.f, 0.f);
 #endif
-    if (c < L) xy[c] = xr[k];
+      if (c < L) xy[c] = xr[k];
+    }
   }
   // picklist entries as wrapped product indices (-1 = out of range)
 #if CO_SLAP_LATE >= 2
@@ -1178,31 +1231,39 @@ extern "C" int co_slap_rollout(int64_t B, int64_t L, int64_t P, int64_t O, int64
   // 8 lanes 33 us, 32 lanes 38 us, at B = 16,384)
   const int G = L <= 64 ? 8 : (L <= 128 ? 16 : 32);
   const int ipb = 256 / G;
+  // LDS-DMA staging of the distance / coordinate rows: 16-byte aligned row blocks
+  const bool sd = CO_SLAP_SD && closest && (L % 4) == 0 &&
+                  ((reinterpret_cast<uintptr_t>(locs) | reinterpret_cast<uintptr_t>(depot_dist)) &
+                   15) == 0;
   const size_t shmem =
-      slap_asg_bytes(ipb, (int)P) + 4 * slap_wave_bytes(64 / G, 8, (int)L, (int)O, (int)K);
+      slap_asg_bytes(ipb, (int)P) +
+      4 * (sd ? slap_wave_bytes_sd(64 / G, 8, (int)L, (int)O, (int)K)
+              : slap_wave_bytes(64 / G, 8, (int)L, (int)O, (int)K));
   if (shmem > 160 * 1024) return CO_E_INVAL;
   const dim3 grid(cover_grid(B, ipb)), block(256);
   if (grid.x == 0) return CO_E_INVAL;
   hipStream_t s = (hipStream_t)stream;
   const float2* l2 = reinterpret_cast<const float2*>(locs);
-#define CO_SLAP(GG, EPL, C)                                                                    \
+#define CO_SLAP(GG, EPL, C, SDD)                                                               \
   do {                                                                                         \
     if (shmem > 64 * 1024)                                                                     \
-      (void)hipFuncSetAttribute((const void*)slap_group_kernel<GG, EPL, C>,                    \
+      (void)hipFuncSetAttribute((const void*)slap_group_kernel<GG, EPL, C, SDD>,               \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);       \
-    hipLaunchKernelGGL((slap_group_kernel<GG, EPL, C>), grid, block, shmem, s, B, (int)L,      \
+    hipLaunchKernelGGL((slap_group_kernel<GG, EPL, C, SDD>), grid, block, shmem, s, B, (int)L, \
                        (int)P, (int)O, (int)K, l2, picklist, depot_dist, assign_in, acts_in,   \
                        acts_out, mask_out, assign_out, i_out, done_out, step_reward_out,       \
                        reward_out, ratio_out, status);                                         \
   } while (0)
-#define CO_SLAP_G(C)                                            \
-  if (G == 8) CO_SLAP(8, 8, C);                                 \
-  else if (G == 16) CO_SLAP(16, 8, C);                          \
-  else CO_SLAP(32, 8, C)
-  if (closest) {
-    CO_SLAP_G(true);
+#define CO_SLAP_G(C, SDD)                                       \
+  if (G == 8) CO_SLAP(8, 8, C, SDD);                            \
+  else if (G == 16) CO_SLAP(16, 8, C, SDD);                     \
+  else CO_SLAP(32, 8, C, SDD)
+  if (closest && sd) {
+    CO_SLAP_G(true, true);
+  } else if (closest) {
+    CO_SLAP_G(true, false);
   } else {
-    CO_SLAP_G(false);
+    CO_SLAP_G(false, false);
   }
 #undef CO_SLAP_G
 #undef CO_SLAP
