@@ -1083,7 +1083,6 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
         env = CVRPEnv(generator_params=dict(num_loc=n), device=dev)
         pol = ConstructivePolicy(None, LogitsDecoder(lambda td: logits), env_name="cvrp")
         steps, calls = [], []
-        real = count_fused_calls(env, calls)
 
         def run():
             td = env.reset(TensorDict(dict(data), [bb]))
@@ -1091,6 +1090,10 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
             steps.append(r["actions"].shape[1])
             return r
 
+        count_fused_calls(env, calls)  # one untimed episode counts the fused launches
+        run()
+        uncount_fused_calls(env)
+        steps.clear()
         wall, ev = timed(run, kk, 2, world, dev)
         t = max_over_ranks(wall, world, dev)
         T = steps[-1]
@@ -1098,12 +1101,11 @@ def bench_dropin_cvrp(b, n, k, world, rank, dev):
             out.update({"value": world * bb * T * kk / t, "ms_per_episode": t / kk * 1e3,
                         "gpu_ms_per_episode": ev / kk * 1e3, "episode_steps": T,
                         "gpu_us_per_step": ev / kk / T * 1e6, "batch_per_gpu": bb,
-                        "launches_per_step": 1 if len(calls) == sum(steps) else 2,
+                        "launches_per_step": 1 if len(calls) == T else 2,
                         "path": "ConstructivePolicy.forward + CVRPEnv "
                                 "(co_cvrp_decode_step per step)"})
         else:
             out["host_us_per_step_b64"] = t / kk / T * 1e6
-        env.decode_and_step, env.native_decode_and_step = real
     out["host_below_kernels"] = out["host_us_per_step_b64"] < out["gpu_us_per_step"]
     out["decode_fused_kernel_us"] = cvrp_decode_step_kernel_us(b, n, dev)
     return out
@@ -1147,7 +1149,9 @@ def cvrp_decode_step_kernel_us(b, n, dev, reps=50):
 
 def count_fused_calls(env, calls):
     """Count the env's fused decode + step calls (the native step glue or the Python
-    decode_and_step); returns the originals to restore."""
+    decode_and_step) by wrapping them on the instance; `uncount_fused_calls(env)` removes
+    the wrappers.  Counting runs one untimed episode: the wrappers add a Python call per
+    step, which the timed episodes must not pay."""
     real = (env.decode_and_step, env.native_decode_and_step)
     env.decode_and_step = lambda *a, **kw: calls.append(1) or real[0](*a, **kw)
     native = real[1]()
@@ -1155,6 +1159,11 @@ def count_fused_calls(env, calls):
         counted = lambda *a, **kw: calls.append(1) or native(*a, **kw)  # noqa: E731
         env.native_decode_and_step = lambda: counted
     return real
+
+
+def uncount_fused_calls(env):
+    for name in ("decode_and_step", "native_decode_and_step"):
+        env.__dict__.pop(name, None)
 
 
 def bench_dropin_slap(b, k, world, rank, dev):
@@ -1194,15 +1203,17 @@ def bench_dropin_slap(b, k, world, rank, dev):
                    else SLAPPointerDecoder(data["locs"], dev))
             pol = ConstructivePolicy(None, dec, env_name="slap", tanh_clipping=10.0)
             calls = []
-            real = count_fused_calls(env, calls)
 
             def run():
                 td = env.reset(TensorDict(dict(data.items()), [bb]))
                 return pol(td, env, phase="test", decode_type="greedy")
 
+            count_fused_calls(env, calls)  # one untimed episode counts the fused launches
+            run()
+            uncount_fused_calls(env)
+            fused_steps = len(calls)
             wall, ev = timed(run, kk, 2, world, dev)
             t = max_over_ranks(wall, world, dev)
-            fused_steps = len(calls) / (kk + 2)
             key = "" if dec_name == "stub" else "am_"
             if bb == b:
                 m = {"value": world * bb * P * kk / t, "ms_per_episode": t / kk * 1e3,
@@ -1218,7 +1229,6 @@ def bench_dropin_slap(b, k, world, rank, dev):
                     out["am_decoder"] = m
             else:
                 out[key + "host_us_per_step_b64"] = t / kk / P * 1e6
-            env.decode_and_step, env.native_decode_and_step = real
             del env, pol, dec, data
     # the marginal host cost of one loop step: episodes of P = 20 and 40 products at B = 64
     # (the per-episode reset / reward / log-likelihood / status read cancel out)

@@ -561,6 +561,32 @@ __global__ __launch_bounds__(64 * CO_ROWS_WPB) void tsp_teacher_rows_kernel(
   }
 }
 
+#ifndef CO_SLAP_CSWAP
+#define CO_SLAP_CSWAP 1  // one-compare comparator (asm selects) in the key sort (r06: -0.5 us)
+#endif
+#ifndef CO_SLAP_KEY2
+#define CO_SLAP_KEY2 1  // distance keys by an add of +0.0 and a sign mask (4 VALU instead of 6;
+                        // r06: -0.7 us at B = 65,536)
+#endif
+#ifndef CO_SLAP_OWNW
+#define CO_SLAP_OWNW 0  // the popping lane writes the assignment; free bits cleared after the
+                        // loop (r06: 43.4 -> 45.3 us at B = 65,536: off)
+#endif
+__device__ __forceinline__ uint32_t sel_u32(uint64_t m, uint32_t t, uint32_t f) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+// compare-exchange with one v_cmp_lt_u64 and four selects on its lane mask (written as
+// two ternaries the compiler emits a second, `gt`, compare for the max)
+__device__ __forceinline__ void cswap_u64(uint64_t& a, uint64_t& b) {
+  const uint64_t lt = __builtin_amdgcn_ballot_w64(a < b);
+  const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b,
+                 bhi = (uint32_t)(b >> 32);
+  a = ((uint64_t)sel_u32(lt, ahi, bhi) << 32) | sel_u32(lt, alo, blo);
+  b = ((uint64_t)sel_u32(lt, bhi, ahi) << 32) | sel_u32(lt, blo, alo);
+}
+
 // ascending sort of EPL u64 keys in registers (Batcher odd-even merge network)
 template <int EPL>
 __device__ __forceinline__ void sort_keys(uint64_t (&k)[EPL]) {
@@ -574,9 +600,13 @@ __device__ __forceinline__ void sort_keys(uint64_t (&k)[EPL]) {
 #pragma unroll
         for (int i = 0; i < q; ++i)
           if (i + j + q < EPL && (i + j) / (2 * p) == (i + j + q) / (2 * p)) {
+#if CO_SLAP_CSWAP
+            cswap_u64(k[i + j], k[i + j + q]);
+#else
             const uint64_t a = k[i + j], b = k[i + j + q];
             k[i + j] = a < b ? a : b;
             k[i + j + q] = a < b ? b : a;
+#endif
           }
 }
 
@@ -799,9 +829,16 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
   if (CLOSEST) {
 #pragma unroll
     for (int k = 0; k < EPL; ++k) {
+#if CO_SLAP_KEY2
+      // -0.0 keyed as +0.0 (d + 0.0 is +0.0 for d = -0.0, d otherwise): they tie as in
+      // argmin's float compare, and the index decides
+      const uint32_t u = __float_as_uint(dd[k] + 0.0f);
+      const uint32_t ord = u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+#else
       // -0.0 keyed as +0.0: they tie (argmin's float compare), the index decides
       const uint32_t u = dd[k] == 0.f ? 0u : __float_as_uint(dd[k]);
       const uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+#endif
       key[k] = ((uint64_t)ord << 32) | (uint32_t)(sl + G * k);
     }
     sort_keys<EPL>(key);
@@ -842,6 +879,32 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
       if (sl == 0) asg[t] = any ? (int32_t)gi : 0;  // product t
     }
 #else
+#if CO_SLAP_OWNW
+    // r06: the owner of the chosen location writes assignment[t] in its pop (a step with no
+    // candidate leaves the pre-stored 0), and the popped keys' free bits are cleared after
+    // the loop from their slots -- 2 VALU and an exec switch fewer per step
+    for (int t = sl; t < P; t += G) asg[t] = 0;
+    uint32_t slots = 0;  // nibble j: the register slot (location / G) of sorted key j
+#pragma unroll
+    for (int j = 0; j < EPL && j < 8; ++j) slots |= (((uint32_t)key[j] - sl) / G) << (4 * j);
+    __builtin_amdgcn_wave_barrier();  // (one wave: the zeros land before any pop's write)
+    for (int t = 0; t < P; ++t) {
+      const uint32_t hh = (uint32_t)(hk >> 32);
+      const uint32_t gm = grp_reduce<G>(hh, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+      const uint32_t cand = hh == gm ? (uint32_t)hk : 0xffffffffu;
+      const uint32_t gi =
+          grp_reduce<G>(cand, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+      if (gm < kOrdInf && (uint32_t)hk == gi) {  // the owner's head is the chosen location
+        asg[t] = (int32_t)gi;  // product t
+        hk = nk;
+        nk = h < EPL ? s_keys[h * 64 + lane] : ~0ull;
+        ++h;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < EPL && j < 8; ++j)
+      if (j < h - 2) avail &= ~(1u << ((slots >> (4 * j)) & 15u));
+#else
     for (int t = 0; t < P; ++t) {
       const uint32_t hh = (uint32_t)(hk >> 32);
       const uint32_t gm = grp_reduce<G>(hh, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
@@ -857,6 +920,7 @@ __global__ __launch_bounds__(256) CO_SLAP_ATTR void slap_group_kernel(
       }
       if (sl == 0) asg[t] = any ? (int32_t)gi : 0;  // product t
     }
+#endif
 #endif
   } else {
     // teacher actions: lane sl loads steps t = sl, sl + G, ... (all loads in flight at
