@@ -71,6 +71,8 @@ elif args.kernel.startswith("tsp"):
                           for _ in range(args.cycle - 1)]
     elif args.kernel == "tsp_fused_nearest":
         ep = engine.TSPFusedEpisode(locs.to(dev), None, policy="nearest")
+    elif args.kernel == "tsp_stepwise_chunked":
+        ep = engine.TSPStepwiseEpisode(locs.to(dev), acts.to(dev), chunk=10)
     else:
         ep = engine.TSPStepwiseEpisode(locs.to(dev), acts.to(dev))
 elif args.kernel.startswith("cvrp"):
