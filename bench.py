@@ -597,6 +597,12 @@ def main():
                     "graph",
         "steps_per_launch": kc, "alg_bytes_per_env_step": swc_bytes,
         "contract_bytes_per_env_step_one_launch_loop": sw_bytes,
+        # PMC (profiles/r*_pmc_traffic.json): inside a launch the L2 absorbs the ping-pong
+        # rewrites (a row's buffer is rewritten every second step), so HBM sees less than
+        # the bytes the kernel issues; the mode is bounded by store issue + launch count
+        "pmc_hbm_bytes_per_env_step_steps_kernel": (
+            lambda t: None if t is None else t / (b * kc))(
+            pmc_traffic("tsp_stepwise_chunked", "tsp_steps_group_kernel<")[0]) if (b, n) == (65536, 100) else None,
         "achieved_GBps": b * n * swc_bytes * k / ev_c / 1e9,
         "frac": b * n * swc_bytes * k / ev_c / 1e9 / HBM_PEAK_GBS,
         "frac_wall": b * n * swc_bytes * k / wall_c / 1e9 / HBM_PEAK_GBS}

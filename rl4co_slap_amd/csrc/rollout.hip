@@ -380,6 +380,13 @@ __host__ __device__ inline size_t tsp_rows_wave_bytes(int gpw, int N) {
 #ifndef CO_ROWS_NTST
 #define CO_ROWS_NTST 1  // non-temporal mask-row stores
 #endif
+#ifndef CO_ROWS_MODE3
+#define CO_ROWS_MODE3 1  // coordinates by LDS-DMA, actions loaded straight into registers
+                         // (r06: half the LDS per wave; 20.7 -> 19.1 us, same-box A/B)
+#endif
+#ifndef CO_ROWS_ANT
+#define CO_ROWS_ANT 0  // MODE 3: the action loads non-temporal (r06: 19.1 -> 35.7 us, partial lines)
+#endif
 template <int G, int EPL, int MODE, bool STATE>
 __global__ __launch_bounds__(64 * CO_ROWS_WPB) void tsp_teacher_rows_kernel(
     int64_t B, int N, const float2* __restrict__ locs, int64_t LB,
@@ -390,14 +397,16 @@ __global__ __launch_bounds__(64 * CO_ROWS_WPB) void tsp_teacher_rows_kernel(
   constexpr int GPW = 64 / G;
   // 16-byte action pairs only when every lane's first step t0 = sl*EPL is even (the row
   // base is 16-byte aligned): an odd EPL takes the scalar loads
-  constexpr bool VEC = MODE == 1 && EPL % 2 == 0, DMA = MODE == 2;
+  // MODE 3: the coordinate rows by LDS-DMA (nt), the actions straight into registers
+  constexpr bool VEC = MODE == 1 && EPL % 2 == 0, DMA = MODE == 2 || MODE == 3,
+                 ADMA = MODE == 2;
   __shared__ uint32_t s_bits[CO_ROWS_WPB][GPW][(G * EPL + 31) / 32];
   extern __shared__ __attribute__((aligned(16))) unsigned char s_rows[];  // DMA: per wave
   constexpr int NWB = (G * EPL + 31) / 32;
   const int lane = lane_id(), sl = lane % G, grp = lane / G, w = wave_in_block();
   uint32_t* bits = s_bits[w][grp];
   const size_t half = DMA ? tsp_rows_wave_bytes(GPW, N) / 2 : 0;
-  unsigned char* s_w = s_rows + (DMA ? (size_t)w * 2 * half : 0);
+  unsigned char* s_w = s_rows + (DMA ? (size_t)w * (ADMA ? 2 : 1) * half : 0);
   const float2* s_xy = reinterpret_cast<const float2*>(s_w);
   const int64_t* s_act = reinterpret_cast<const int64_t*>(s_w + half);
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + w;
@@ -418,20 +427,28 @@ __global__ __launch_bounds__(64 * CO_ROWS_WPB) void tsp_teacher_rows_kernel(
       const int64_t lb = LB == B ? base : base % LB;
       wave_dma<CO_ROWS_AUX>(reinterpret_cast<const unsigned char*>(locs + lb * N), rows * N * 8,
                             s_w);
-      wave_dma<CO_ROWS_AUX>(reinterpret_cast<const unsigned char*>(acts + base * (int64_t)N),
-                            rows * N * 8, s_w + half);
+      if constexpr (ADMA)
+        wave_dma<CO_ROWS_AUX>(reinterpret_cast<const unsigned char*>(acts + base * (int64_t)N),
+                              rows * N * 8, s_w + half);
+    }
+    int64_t av[EPL];
+    if constexpr (MODE == 3) {  // in flight with the DMA; slots past N re-read step N-1
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) av[k] = ld_s<CO_ROWS_ANT>(arow + (t0 + k < N ? t0 + k : N - 1));
+    }
+    if constexpr (DMA) {
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     // the lane's EPL actions: 16-byte vectors when the row is 16-byte aligned
-    int64_t av[EPL];
-    if constexpr (DMA) {
+    if constexpr (ADMA) {
       // branch-free: slots past N re-read step N-1 (in the staged block); their
       // contributions are masked below
 #pragma unroll
       for (int k = 0; k < EPL; ++k) av[k] = s_act[grp * N + (t0 + k < N ? t0 + k : N - 1)];
+    } else if constexpr (MODE == 3) {
     } else if constexpr (VEC) {
 #pragma unroll
       for (int k = 0; k < EPL; k += 2) {
@@ -1154,7 +1171,12 @@ int launch_tsp_rows(int64_t B, int64_t N, const float2* l2, int64_t LB, const in
     const size_t dsh = WPB * tsp_rows_wave_bytes(64 / GG, (int)N);                             \
     /* the static visited bitmaps come on top of the dynamic staging (64 KiB default) */       \
     const size_t sbits = (size_t)WPB * (64 / GG) * ((GG * EE + 31) / 32) * 4;                  \
-    if (dma_ok && (LB == B || LB % (64 / GG) == 0) && dsh + sbits <= 64 * 1024)                \
+    if (CO_ROWS_MODE3 && dma_ok && (LB == B || LB % (64 / GG) == 0) &&                       \
+        dsh / 2 + sbits <= 64 * 1024)                                                          \
+      hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 3, STATE>), grid, block, dsh / 2, s,  \
+                         B, (int)N, l2, LB, acts, sb, mask_out, first_out, cur_out, i_out,     \
+                         done_out, step_reward_out, reward_out, check, status);                \
+    else if (dma_ok && (LB == B || LB % (64 / GG) == 0) && dsh + sbits <= 64 * 1024)           \
       hipLaunchKernelGGL((tsp_teacher_rows_kernel<GG, EE, 2, STATE>), grid, block, dsh, s, B,   \
                          (int)N, l2, LB, acts, sb, mask_out, first_out, cur_out, i_out,        \
                          done_out, step_reward_out, reward_out, check, status);                \
