@@ -384,6 +384,9 @@ __host__ __device__ inline size_t tsp_rows_wave_bytes(int gpw, int N) {
 #define CO_ROWS_MODE3 1  // coordinates by LDS-DMA, actions loaded straight into registers
                          // (r06: half the LDS per wave; 20.7 -> 19.1 us, same-box A/B)
 #endif
+#ifndef CO_ROWS_AV4
+#define CO_ROWS_AV4 0  // MODE 3: the actions as 16-byte pieces (odd EPL; r06: no faster, off)
+#endif
 #ifndef CO_ROWS_ANT
 #define CO_ROWS_ANT 0  // MODE 3: the action loads non-temporal (r06: 19.1 -> 35.7 us, partial lines)
 #endif
@@ -432,9 +435,25 @@ __global__ __launch_bounds__(64 * CO_ROWS_WPB) void tsp_teacher_rows_kernel(
                               rows * N * 8, s_w + half);
     }
     int64_t av[EPL];
-    if constexpr (MODE == 3) {  // in flight with the DMA; slots past N re-read step N-1
+    if constexpr (MODE == 3) {  // in flight with the DMA
+      if constexpr (CO_ROWS_AV4 && EPL % 2 == 1) {
+        // 16-byte pieces (8-byte aligned: gfx950 loads them whole), branch-free and inside
+        // the row: pair j starts at p = min(t0 + 2j, N - 2); when clamped, step t0 + 2j is
+        // N - 1 (its .y) or past N (masked below like every slot past N)
+        typedef long long i64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
 #pragma unroll
-      for (int k = 0; k < EPL; ++k) av[k] = ld_s<CO_ROWS_ANT>(arow + (t0 + k < N ? t0 + k : N - 1));
+        for (int k = 0; k + 1 < EPL; k += 2) {
+          const int p = t0 + k < N - 2 ? t0 + k : N - 2;
+          const i64x2a8 v = *reinterpret_cast<const i64x2a8*>(arow + p);
+          av[k] = p == t0 + k ? v.x : v.y;
+          av[k + 1] = v.y;
+        }
+        av[EPL - 1] = arow[t0 + EPL - 1 < N ? t0 + EPL - 1 : N - 1];
+      } else {  // slots past N re-read step N-1
+#pragma unroll
+        for (int k = 0; k < EPL; ++k)
+          av[k] = ld_s<CO_ROWS_ANT>(arow + (t0 + k < N ? t0 + k : N - 1));
+      }
     }
     if constexpr (DMA) {
       __builtin_amdgcn_s_waitcnt(0);
