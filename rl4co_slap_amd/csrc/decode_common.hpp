@@ -967,7 +967,14 @@ __global__ __launch_bounds__(256) void tsp_decode_step_kernel(
 // Greedy decode step fused with TSPEnv._step on the GreedyRow engine (the POMO /
 // multistart-greedy hot loop); same outputs as tsp_decode_step_kernel in greedy mode.
 // The mask words are updated in registers (the selected byte cleared) and stored back.
-template <int RL, int EPL, int VW, int OPT>
+// STAGE (round 6): the wave's RPW logits rows and mask rows (contiguous: lstride == N,
+// N % 4 == 0, 16-byte aligned) arrive by non-temporal LDS-DMA -- whole-line streams --
+// and the lanes read their chunks from LDS; the certified fallback re-reads the row from
+// memory as before.
+__host__ __device__ inline size_t tsp_dstage_bytes(int rpw, int N) {
+  return (size_t)rpw * N * 4 + (((size_t)rpw * N + 15) & ~(size_t)15);
+}
+template <int RL, int EPL, int VW, int OPT, bool STAGE = false>
 __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     int64_t B, int N, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int64_t* __restrict__ action_out,
@@ -977,6 +984,7 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     uint8_t* __restrict__ step_reward, float* __restrict__ ll_accum, int32_t* status) {
   constexpr int RPW = 64 / RL;
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dstage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
   const unsigned long long gmask = RL == 64 ? ~0ull : (((1ull << RL) - 1ull) << (grp * RL));
@@ -998,7 +1006,17 @@ __global__ __launch_bounds__(256) void tsp_decode_greedy_kernel(
     GreedyRow<RL, EPL, VW> g;
     const float* lrow = logits + r * lstride;
     const uint8_t* mrow = mask_in + r * (int64_t)N;
-    g.load(valid, N, lrow, mrow, c0);
+    if constexpr (STAGE) {
+      const int nr = (int)(B - base < RPW ? B - base : RPW);
+      unsigned char* sw = s_dstage + (size_t)wave_in_block() * tsp_dstage_bytes(RPW, N);
+      wave_dma<2>(reinterpret_cast<const unsigned char*>(logits + base * N), nr * N * 4, sw);
+      wave_dma<2>(mask_in + base * N, nr * N, sw + (size_t)RPW * N * 4);
+      wave_dma_wait();
+      g.load(valid, N, reinterpret_cast<const float*>(sw) + grp * N, sw + (size_t)RPW * N * 4 + grp * N,
+             c0);
+    } else {
+      g.load(valid, N, lrow, mrow, c0);
+    }
     float lp, L;
     const int sel = greedy_row<OPT>(g, valid, N, clip, temp, sl, c0,
                                            group_scratch<RL, EPL>(lds, grp), L, lp, lrow, mrow);

@@ -19,6 +19,11 @@
 // (co_decode_step + co_slap_step / co_cvrp_step) bit for bit, RNG use included.
 #include "decode_common.hpp"
 
+#ifndef CO_DECODE_STAGE
+#define CO_DECODE_STAGE 0  // rows by non-temporal LDS-DMA (r06: TSP decode step 16.0 -> 17.9 us,
+                           // SLAP 12.1 -> 13.0 us at B = 65,536: off)
+#endif
+
 namespace {
 
 // ------------------------------------------------------------------ env staging
@@ -134,7 +139,9 @@ struct SlapStage {
 };
 
 // Greedy (GreedyRow; certified / exact / fast per OPT) decode + SLAP step.
-template <int RL, int EPL, int VW, int OPT>
+// STAGE (round 6): the wave's logits and mask rows (contiguous, 16-byte aligned) by
+// non-temporal LDS-DMA after the env stage, read from LDS (tsp_decode_greedy_kernel's form)
+template <int RL, int EPL, int VW, int OPT, bool STAGE = false>
 __global__ __launch_bounds__(256) void slap_decode_greedy_kernel(
     int64_t B, int L, const float* __restrict__ logits, int64_t lstride,
     const uint8_t* __restrict__ mask_in, float clip, float temp, int64_t* __restrict__ action_out,
@@ -143,7 +150,11 @@ __global__ __launch_bounds__(256) void slap_decode_greedy_kernel(
   __shared__ __attribute__((aligned(16))) float lds[4 * 64 * EPL];
   extern __shared__ __attribute__((aligned(16))) uint32_t s_stage[];
   const int lane = lane_id(), sl = lane % RL, grp = lane / RL, c0 = sl * EPL;
-  const SlapStage<RL> st{s_stage + wave_in_block() * slap_stage_dwords(RPW, e.P), e.P};
+  const size_t wstage = STAGE ? ((size_t)slap_stage_dwords(RPW, e.P) * 4 + 15) & ~(size_t)15
+                              : (size_t)slap_stage_dwords(RPW, e.P) * 4;
+  const size_t wbytes = wstage + (STAGE ? tsp_dstage_bytes(RPW, L) : 0);
+  unsigned char* wbase_lds = reinterpret_cast<unsigned char*>(s_stage) + wave_in_block() * wbytes;
+  const SlapStage<RL> st{reinterpret_cast<uint32_t*>(wbase_lds), e.P};
   // one row group per wave (the grid covers B: no loop, so nothing is hoisted into
   // registers across row groups)
   const int64_t wid = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave_in_block();
@@ -158,7 +169,16 @@ __global__ __launch_bounds__(256) void slap_decode_greedy_kernel(
     GreedyRow<RL, EPL, VW> g;
     const float* lrow = logits + r * lstride;
     const uint8_t* mrow = mask_in + r * (int64_t)L;
-    g.load(valid, L, lrow, mrow, c0);
+    if constexpr (STAGE) {
+      unsigned char* sw = wbase_lds + wstage;
+      wave_dma<2>(reinterpret_cast<const unsigned char*>(logits + base * L), nr * L * 4, sw);
+      wave_dma<2>(mask_in + base * L, nr * L, sw + (size_t)RPW * L * 4);
+      wave_dma_wait();
+      g.load(valid, L, reinterpret_cast<const float*>(sw) + grp * L,
+             sw + (size_t)RPW * L * 4 + grp * L, c0);
+    } else {
+      g.load(valid, L, lrow, mrow, c0);
+    }
     float lp, lse;
     const int sel = greedy_row<OPT>(g, valid, L, clip, temp, sl, c0,
                                     group_scratch<RL, EPL>(lds, grp), lse, lp, lrow, mrow);
@@ -535,6 +555,20 @@ extern "C" int co_slap_decode_step(int64_t B, int64_t L, int64_t P, const float*
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid(cover_grid(B, rpw * 4)), block(256);
   if (grid.x == 0) return CO_E_INVAL;
+  if (mode == CO_DECODE_GREEDY && CO_DECODE_STAGE && N > 64 && N <= 128 && N % 4 == 0 &&
+      lstride == N && greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr) == 4 &&
+      ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(mask_in)) & 15) == 0) {
+    // the logits and mask rows by non-temporal LDS-DMA (slap_decode_greedy_kernel STAGE)
+    const size_t wst = (((size_t)slap_stage_dwords(rpw, (int)P) * 4 + 15) & ~(size_t)15) +
+                       tsp_dstage_bytes(rpw, (int)N);
+    if (4 * wst + lds_static <= 64 * 1024) {
+      CO_OPT_DISPATCH_G(hipLaunchKernelGGL,
+                        (slap_decode_greedy_kernel<CO_RL128, 128 / CO_RL128, 4, OPT, true>), grid,
+                        block, 4 * wst, s, B, (int)N, logits, lstride, mask_in, clip, temp,
+                        action_out, logp_sel, status, epi);
+      return launch_status();
+    }
+  }
   if (mode == CO_DECODE_GREEDY) {
 #define CO_SDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \

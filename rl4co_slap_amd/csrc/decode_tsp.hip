@@ -1,6 +1,10 @@
 // co_tsp_decode_step: the decode step fused with TSPEnv._step (decode_common.hpp engines).
 #include "decode_common.hpp"
 
+#ifndef CO_DECODE_STAGE
+#define CO_DECODE_STAGE 0  // rows by non-temporal LDS-DMA (r06: TSP decode 16.0 -> 17.9 us: off)
+#endif
+
 extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int64_t lstride,
                                   const uint8_t* mask_in, float clip, float temp, int mode,
                                   const int64_t* action_in, int64_t* action_out,
@@ -23,6 +27,19 @@ extern "C" int co_tsp_decode_step(int64_t B, int64_t N, const float* logits, int
   if (mode == CO_DECODE_GREEDY) {
     const dim3 grid(decode_grid(B, (int)N)), block(256);
     if (grid.x == 0) return CO_E_INVAL;
+    // the row-group width of 64 < N <= 128 with contiguous, 16-byte aligned rows: the
+    // logits and mask rows by non-temporal LDS-DMA (tsp_decode_greedy_kernel STAGE)
+    if (CO_DECODE_STAGE && N > 64 && N <= 128 && N % 4 == 0 && lstride == N &&
+        greedy_vw(N, lstride, logits, mask_in, mask_out, nullptr) == 4 &&
+        ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(mask_in)) & 15) == 0) {
+      const size_t dsh = 4 * tsp_dstage_bytes(64 / CO_RL128, (int)N);
+      CO_OPT_DISPATCH_G(hipLaunchKernelGGL,
+                        (tsp_decode_greedy_kernel<CO_RL128, 128 / CO_RL128, 4, OPT, true>), grid,
+                        block, dsh, s, B, (int)N, logits, lstride, mask_in, clip, temp, action_out,
+                        logp_sel, mask_out, i_in, i_out, first_in, first_out, first_mode, done,
+                        step_reward, ll_accum, status);
+      return launch_status();
+    }
 #define CO_TDG(RL, EPL, V)                                                                     \
   CO_OPT_DISPATCH_G(hipLaunchKernelGGL,                                                        \
                     (tsp_decode_greedy_kernel<RL, (EPL < 4 ? 4 : EPL), V, OPT>), grid, block, 0, \

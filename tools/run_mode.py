@@ -68,6 +68,8 @@ def main():
         out = bench.bench_dropin_cvrp(32768, 100, a.k, 1, 0, dev)
     elif a.mode == "dropin_slap":
         out = bench.bench_dropin_slap(16384, a.k, 1, 0, dev)
+    elif a.mode == "slap_decode_kernels":  # the fused SLAP decode step alone, B = 16,384 / 65,536
+        out = {b: round(bench.slap_decode_step_kernel_us(b, dev), 3) for b in (16384, 65536)}
     elif a.mode == "pomo":
         out = bench.bench_pomo(1024, 100, a.k, 1, 0, dev)
     elif a.mode == "pomo_cert":
