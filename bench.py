@@ -624,7 +624,10 @@ def main():
         "stepwise": {"value": sc["value"], "ms_per_episode": sc["ms_per_episode"],
                      "launches_per_step": 1, "policy": sc["policy"],
                      "alg_bytes_per_env_step": 234 + 1684 / 20,
-                     "frac_wall": sc["value"] / world * (234 + 1684 / 20) / 1e9 / HBM_PEAK_GBS}}
+                     "frac_wall": sc["value"] / world * (234 + 1684 / 20) / 1e9 / HBM_PEAK_GBS},
+        "stepwise_chunked": {k_: slap65["slap_stepwise_chunked"][k_] for k_ in (
+            "value", "ms_per_episode", "steps_per_launch", "alg_bytes_per_env_step", "frac",
+            "frac_wall")}}
 
     if not args.no_modes:
         modes = {}
@@ -893,6 +896,18 @@ def annotate_modes(modes, n, world):
                 m["sq_issue_frac"], m["sq_issue_source"] = sq
 
 
+SLAP_CHUNK = 10
+
+
+def slap_chunk_bytes(kc, L=100, P=20):
+    """Algorithmic HBM bytes per env-step of the chunked closest-free SLAP episode: every
+    step writes the mask row L, i 8, done + reward 2, its action 8 and assignment entry 4
+    and reads its product 4; each launch reads the row's depot distances 4L, mask L and i
+    8 once; the first step's out-of-place assignment row (read + write 8P) and the
+    episode's reset + pick-tour reward (1684 B) amortised over the P steps."""
+    return L + 26 + (5 * L + 8) / kc + (8 * P + 1684) / P
+
+
 def bench_slap(b, k, world, rank, dev, stepwise=True):
     import numpy as np
 
@@ -947,6 +962,19 @@ def bench_slap(b, k, world, rank, dev, stepwise=True):
     out["slap_stepwise_graph"] = {"value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3,
                                   "batch_per_gpu": b, "bytes_per_env_step": 234,
                                   "launches_per_step": 1, "policy": "closest-free (fused)"}
+    del ep
+    # the same policy and per-step state writes, SLAP_CHUNK steps per co_slap_closest_steps
+    # launch (the row's distances and mask in registers across the chunk)
+    ep = SLAPStepwiseEpisode(td, policy="closest", chunk=SLAP_CHUNK).capture()
+    wall, ev = timed(ep.replay, k, 2, world, dev)
+    assert int(ep.status.item()) == 0, "SLAP chunked stepwise episode status"
+    t = max_over_ranks(wall, world, dev)
+    out["slap_stepwise_chunked"] = {
+        "value": world * b * 20 * k / t, "ms_per_episode": t / k * 1e3, "batch_per_gpu": b,
+        "steps_per_launch": SLAP_CHUNK, "policy": "closest-free (fused)",
+        "alg_bytes_per_env_step": slap_chunk_bytes(SLAP_CHUNK),
+        "frac_wall": b * 20 * slap_chunk_bytes(SLAP_CHUNK) * k / wall / 1e9 / HBM_PEAK_GBS,
+        "frac": b * 20 * slap_chunk_bytes(SLAP_CHUNK) * k / ev / 1e9 / HBM_PEAK_GBS}
     del ep
     # the env step alone (co_slap_step), teacher-forced random-feasible actions
     torch.manual_seed(4321 + rank)

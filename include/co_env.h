@@ -314,6 +314,20 @@ int co_slap_closest_step(int64_t batch, int64_t num_slots, int64_t n_products,
                          int64_t* action_out, const int64_t* i_in, int64_t* i_out, uint8_t* done,
                          uint8_t* reward, int32_t* status, void* stream);
 
+/* K consecutive co_slap_closest_step calls in one launch (round 6): the state ping-pongs
+ * between buffers A and B (step k reads mask / i from A for even k, from B for odd k, and
+ * writes the other), step k's action to action_out + k*act_stride, its product from
+ * to_choose column k (row stride tc_stride; with to_choose NULL the uniform product
+ * tc_stride + k), the assignment of step 0 written out of place from assign_in when it
+ * differs from assign_out and in place after; done / reward written by every step.  Each
+ * step stores its whole state as its own launch would; the final contents are
+ * bit-identical to the K calls.  For the stepwise engine's closest-free bench policy. */
+int co_slap_closest_steps(int64_t batch, int64_t num_slots, int64_t n_products, int64_t steps,
+                          const float* depot_loc_dist, const float* to_choose, int64_t tc_stride,
+                          const int32_t* assign_in, int32_t* assign_out, uint8_t* mask_a,
+                          int64_t* i_a, uint8_t* mask_b, int64_t* i_b, int64_t* action_out,
+                          int64_t act_stride, uint8_t* done, uint8_t* reward, int32_t* status,
+                          void* stream);
 
 /* -------------------------------------------- fused episode rollouts */
 

@@ -29,6 +29,8 @@ _SIGS = {
     "co_tsp_reset": [_i64, _i64, _p, _p, _p, _p, _p, _p],
     "co_tsp_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p, _p],
     "co_tsp_steps": [_i64, _i64, _i64, _p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i32, _p, _p],
+    "co_slap_closest_steps": [_i64, _i64, _i64, _i64, _p, _p, _i64, _p, _p, _p, _p, _p, _p, _p,
+                              _i64, _p, _p, _p, _p],
     "co_tsp_reward": [_i64, _i64, _i64, _p, _i64, _p, _i64, _i64, _i32, _p, _p, _p],
     "co_cvrp_reset": [_i64, _i64, _p, _p, _p, _f32, _p, _p, _p, _p, _p, _p, _p],
     "co_cvrp_step": [_i64, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],

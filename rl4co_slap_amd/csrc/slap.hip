@@ -486,7 +486,140 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
   }
 }
 
+// K consecutive co_slap_closest_step launches in one (co_slap_closest_steps, round 6): the
+// state ping-pongs between A and B (step k reads A for even k, B for odd k, writes the
+// other), step k's action goes to row k of action_out, its product to_choose column k
+// (the uniform product tc_stride + k without to_choose), the assignment of step 0 out of
+// place from assign_in when it differs from assign, then in place; every step stores its
+// whole state as its own launch would.  The row's distances and mask units stay in
+// registers between steps; the group argmin is the single step's.
+template <int KU>
+__global__ __launch_bounds__(256) void slap_closest_steps_kernel(
+    int64_t B, int L, int P, int K, const float* __restrict__ dist, const float* to_choose,
+    int64_t tc_stride, const int32_t* assign_in, int32_t* assign, uint8_t* mask_a,
+    int64_t* i_a, uint8_t* mask_b, int64_t* i_b, int64_t* __restrict__ action_out,
+    int64_t astride, uint8_t* __restrict__ done, uint8_t* __restrict__ reward, int32_t* status) {
+  constexpr int G = 16;
+  const int sl = threadIdx.x & (G - 1);
+  const int64_t b = (int64_t)blockIdx.x * (256 / G) + (threadIdx.x / G);
+  const bool live = b < B;
+  const int64_t bb = live ? b : B - 1;  // dead groups mirror the last row (wave-uniform DPP)
+  const int U = L >> 2;
+  const float4* drow = reinterpret_cast<const float4*>(dist + bb * (int64_t)L);
+  const uint32_t* mrow = reinterpret_cast<const uint32_t*>(mask_a + bb * (int64_t)L);
+  float4 dv[KU];
+  uint32_t mv[KU];
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    const int u = sl + G * k;
+    const int uc = u < U ? u : U - 1;
+    dv[k] = drow[uc];
+    mv[k] = mrow[uc];
+  }
+  int64_t it = i_a[bb];  // (every lane: one broadcast line)
+  bool range = false;
+  for (int t = 0; t < K; ++t) {
+    const float prod = to_choose ? to_choose[bb * tc_stride + t] : (float)(tc_stride + t);
+    float best = __builtin_inff();
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+      const int u = sl + G * k;
+      if (u < U) {
+        const float d4[4] = {dv[k].x, dv[k].y, dv[k].z, dv[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = ((mv[k] >> (8 * j)) & 0xffu) ? d4[j] : __builtin_inff();
+          if (d < best) {
+            best = d;
+            bi = 4 * u + j;
+          }
+        }
+        if (bi == 0x7fffffff) bi = 4 * u;
+      }
+    }
+    grp_argmin_split<G>(best, bi);
+    const bool to_b = (t & 1) == 0;
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+      const int u = sl + G * k;
+      const uint32_t clr = (bi >> 2) == u ? ~(0xffu << (8 * (bi & 3))) : ~0u;
+      mv[k] &= clr;
+    }
+    if (live) {
+      int64_t p = (int64_t)(int)prod;  // .to(torch.int), slap/env.py:52
+      if (p < 0) p += P;
+      const bool p_ok = p >= 0 && p < P;
+      if (t == 0 && assign_in != assign)  // out of place: the row with [p] = action
+        for (int c = sl; c < P; c += G) assign[b * P + c] = c == p ? (int32_t)bi : assign_in[b * P + c];
+      uint32_t* mo = reinterpret_cast<uint32_t*>((to_b ? mask_b : mask_a) + b * (int64_t)L);
+#pragma unroll
+      for (int k = 0; k < KU; ++k) {
+        const int u = sl + G * k;
+        if (u < U) mo[u] = mv[k];
+      }
+      if (sl == 0) {
+        action_out[(int64_t)t * astride + b] = bi;
+        if (!p_ok)
+          range = true;
+        else if (t > 0 || assign_in == assign)
+          assign[b * P + p] = (int32_t)bi;
+        done[b] = it == (int64_t)(P - 1);
+        (to_b ? i_b : i_a)[b] = it + 1;
+        reward[b] = 0;
+      }
+    }
+    it += 1;
+  }
+  if (range) set_status(status, CO_ST_INDEX_RANGE);
+}
+
 }  // namespace
+
+extern "C" int co_slap_closest_steps(int64_t B, int64_t L, int64_t P, int64_t K,
+                                     const float* dist, const float* to_choose, int64_t tc_stride,
+                                     const int32_t* assign_in, int32_t* assign, uint8_t* mask_a,
+                                     int64_t* i_a, uint8_t* mask_b, int64_t* i_b,
+                                     int64_t* action_out, int64_t act_stride, uint8_t* done,
+                                     uint8_t* reward, int32_t* status, void* stream) {
+  if (B < 0 || L <= 0 || P <= 0 || L > (1 << 30) || K < 0 || K > (1 << 20)) return CO_E_INVAL;
+  if (B == 0 || K == 0) return CO_OK;
+  if (!dist || !assign_in || !assign || !mask_a || !i_a || !mask_b || !i_b || !action_out ||
+      act_stride < B || !done || !reward || !status ||
+      (!to_choose && (tc_stride < 0 || tc_stride + K > P)))
+    return CO_E_INVAL;
+  const bool vec = L % 4 == 0 && L <= 4 * 16 * 4 &&
+                   ((reinterpret_cast<uintptr_t>(dist) & 15) |
+                    ((reinterpret_cast<uintptr_t>(mask_a) | reinterpret_cast<uintptr_t>(mask_b)) &
+                     3)) == 0;
+  if (!vec) {  // the K single steps
+    for (int64_t t = 0; t < K; ++t) {
+      const bool even = (t & 1) == 0;
+      const int rc = co_slap_closest_step(
+          B, L, P, dist, to_choose ? to_choose + t : nullptr, to_choose ? tc_stride : tc_stride + t,
+          t == 0 ? assign_in : assign, assign, even ? mask_a : mask_b, even ? mask_b : mask_a,
+          action_out + t * act_stride, even ? i_a : i_b, even ? i_b : i_a, done, reward, status,
+          stream);
+      if (rc != CO_OK) return rc;
+    }
+    return CO_OK;
+  }
+  const dim3 grid(cover_grid(B, 16));
+  if (grid.x == 0) return CO_E_INVAL;
+  const int units = (int)(L / 4), ku = (units + 15) / 16;
+#define CO_SLAP_CSS(KK)                                                                        \
+  hipLaunchKernelGGL((slap_closest_steps_kernel<KK>), grid, dim3(256), 0, (hipStream_t)stream, \
+                     B, (int)L, (int)P, (int)K, dist, to_choose, tc_stride, assign_in, assign,  \
+                     mask_a, i_a, mask_b, i_b, action_out, act_stride, done, reward, status)
+  switch (ku) {
+    case 1: CO_SLAP_CSS(1); break;
+    case 2: CO_SLAP_CSS(2); break;
+    case 3: CO_SLAP_CSS(3); break;
+    default: CO_SLAP_CSS(4);
+  }
+#undef CO_SLAP_CSS
+  return launch_status();
+}
 
 extern "C" int co_slap_reset(int64_t B, int64_t L, int64_t P, uint8_t* mask, float* to_choose,
                              int64_t* it, float* reward, float* ratio, uint8_t* done,

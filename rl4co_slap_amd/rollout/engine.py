@@ -122,15 +122,20 @@ class TSPStepwiseEpisode(_GraphEpisode):
 class SLAPStepwiseEpisode(_GraphEpisode):
     """Reset + P x co_slap_step (in-place assignment) + co_slap_reward; with the
     closest-free bench policy each step is one co_slap_closest_step launch (policy +
-    step), teacher-forced actions go through co_slap_step alone."""
+    step), teacher-forced actions go through co_slap_step alone.
 
-    def __init__(self, td, actions=None, policy: str = "teacher"):
+    ``chunk`` > 1 (closest policy): the steps go out as ceil(P / chunk)
+    co_slap_closest_steps launches -- the same per-step state writes into the same
+    ping-pong buffers (bit-identical), fewer launch boundaries."""
+
+    def __init__(self, td, actions=None, policy: str = "teacher", chunk: int = 1):
         locs = td["locs"]
         super().__init__(locs.device)
         d = locs.device
         b, l = locs.shape[0], locs.shape[1]
         p = td["freq"].shape[-2]
         self.b, self.l, self.p, self.policy = b, l, p, policy
+        self.chunk = max(1, int(chunk)) if policy == "closest" else 1
         self.locs = locs.contiguous()
         self.picklist = td["picklist"].contiguous()
         self.depot_dist = td["depot_loc_dist"].contiguous()
@@ -155,7 +160,16 @@ class SLAPStepwiseEpisode(_GraphEpisode):
         nat.call("co_slap_reset", b, l, p, nat.ptr(self.mask[0]), nat.ptr(self.to_choose),
                  nat.ptr(self.i[0]), nat.ptr(self.reset_reward), nat.ptr(self.ratio), None, None,
                  s)
-        for t in range(p):
+        for t0 in range(0, p if self.chunk > 1 else 0, self.chunk):
+            k = min(self.chunk, p - t0)
+            a_, b_ = t0 & 1, (t0 + 1) & 1  # step t0 reads buffer a_ (the ping-pong parity)
+            nat.call("co_slap_closest_steps", b, l, p, k, nat.ptr(self.depot_dist),
+                     nat.ptr(self.to_choose[:, t0:]), p,
+                     nat.ptr(self.assign0 if t0 == 0 else self.assign), nat.ptr(self.assign),
+                     nat.ptr(self.mask[a_]), nat.ptr(self.i[a_]), nat.ptr(self.mask[b_]),
+                     nat.ptr(self.i[b_]), nat.ptr(self.acts[t0]), b, nat.ptr(self.done),
+                     nat.ptr(self.step_reward), nat.ptr(self.status), s)
+        for t in range(p if self.chunk == 1 else 0):
             src, dst = t & 1, (t + 1) & 1
             a = self.acts[t]
             tc = self.to_choose[:, t:]
@@ -250,6 +264,7 @@ class SLAPFusedEpisode(_GraphEpisode):
         b, l = locs.shape[0], locs.shape[1]
         p = td["freq"].shape[-2]
         self.b, self.l, self.p, self.policy = b, l, p, policy
+        self.chunk = max(1, int(chunk)) if policy == "closest" else 1
         # co_slap_rollout holds an instance's L locations in 8 registers of up to 32 lanes
         # (L <= 256); larger warehouses run the same episode as the stepwise launch sequence
         self._stepwise = SLAPStepwiseEpisode(td, actions, policy) if l > 256 else None

@@ -68,6 +68,20 @@ def main():
         out = bench.bench_dropin_cvrp(32768, 100, a.k, 1, 0, dev)
     elif a.mode == "dropin_slap":
         out = bench.bench_dropin_slap(16384, a.k, 1, 0, dev)
+    elif a.mode == "slap_chunks":  # closest-free stepwise SLAP at B = 65,536, chunk sweep
+        from rl4co_slap_amd.envs.slap import SLAPGenerator
+        from rl4co_slap_amd.rollout.engine import SLAPStepwiseEpisode
+
+        torch.manual_seed(1234)
+        td = SLAPGenerator(materialize_dist_mat=False)(65536).to(dev)
+        out = {}
+        for c in (1, 2, 4, 5, 10, 20):
+            ep = SLAPStepwiseEpisode(td, policy="closest", chunk=c).capture()
+            wall, ev = bench.timed(ep.replay, a.k, 2, 1, dev)
+            byts = bench.slap_chunk_bytes(c) if c > 1 else 234 + 1684 / 20
+            out[c] = {"us_per_episode": round(wall / a.k * 1e6, 2),
+                      "frac_wall": round(65536 * 20 * byts * a.k / wall / 1e9 / bench.HBM_PEAK_GBS, 4)}
+            del ep
     elif a.mode == "slap_decode_kernels":  # the fused SLAP decode step alone, B = 16,384 / 65,536
         out = {b: round(bench.slap_decode_step_kernel_us(b, dev), 3) for b in (16384, 65536)}
     elif a.mode == "pomo":
