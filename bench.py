@@ -741,6 +741,11 @@ def summarize(out):
                                    "frac": r(t["roofline"]["frac"])}
         sm["slap_b65536_stepwise"] = {"env_steps_s": r(t["stepwise"]["value"], 0),
                                       "frac_wall": r(t["stepwise"]["frac_wall"])}
+        if "stepwise_chunked" in t:
+            c = t["stepwise_chunked"]
+            sm["slap_b65536_stepwise_chunked"] = {
+                "env_steps_s": r(c["value"], 0), "frac": r(c["frac"]),
+                "frac_wall": r(c["frac_wall"]), "steps_per_launch": c["steps_per_launch"]}
     # the same run's streaming ceiling (co_probe_copy of 2 GiB): each rate below also as a
     # fraction of it, so a box that streams slower shows up here, not as a regression
     cp = out["roofline"].get("copy_probe", {})
