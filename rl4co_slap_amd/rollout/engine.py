@@ -264,7 +264,6 @@ class SLAPFusedEpisode(_GraphEpisode):
         b, l = locs.shape[0], locs.shape[1]
         p = td["freq"].shape[-2]
         self.b, self.l, self.p, self.policy = b, l, p, policy
-        self.chunk = max(1, int(chunk)) if policy == "closest" else 1
         # co_slap_rollout holds an instance's L locations in 8 registers of up to 32 lanes
         # (L <= 256); larger warehouses run the same episode as the stepwise launch sequence
         self._stepwise = SLAPStepwiseEpisode(td, actions, policy) if l > 256 else None
