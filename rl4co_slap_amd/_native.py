@@ -328,6 +328,7 @@ class _TorchStep:
         self.slap_reset_td = bound(mod.slap_reset_td, "co_slap_reset")
         self.episode_stack = bound(mod.episode_stack, "co_episode_stack")
         self.slab_fresh = mod.slab_fresh
+        self.fast_step = getattr(mod, "fast_step", None)
         self.clear_pool = mod.clear_pool
         self.set_inplace = mod.set_inplace
         self.inplace_policy = mod.inplace_policy

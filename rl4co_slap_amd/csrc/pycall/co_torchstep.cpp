@@ -1077,6 +1077,79 @@ PyObject* inplace_policy(PyObject*, PyObject* const*, Py_ssize_t) {
   return Py_BuildValue("(OO)", kInplaceBuild ? Py_True : Py_False, g_inplace ? Py_True : Py_False);
 }
 
+// fast_step(native, td_type, mword, temp, clip, status, key, actions, logprobs, strategy,
+//           idx_attr, check_rc, td, logits, mask) -> bool
+// The per-step closure of DecodingStrategy.fast_stepper (utils/decoding.py) in C, bound
+// with functools.partial over everything but (td, logits, mask): False, having done
+// nothing, when td is not of td_type or mask is not the td's action_mask (the caller then
+// takes step_env_fused); else native(td, logits, mword, temp, clip, None, 0,
+// strategy.<idx_attr>, status, key) -- an env's *_step_td glue -- whose None also means
+// False and whose int status goes to check_rc("decode_and_step", rc); then
+// strategy.<idx_attr> += 1 and the (action, logp) pair appended to the two lists.  The
+// same calls in the same order as the Python closure, without its frame per step.
+PyObject* fast_step(PyObject*, PyObject* const* a, Py_ssize_t n) {
+  if (n != 15) {
+    PyErr_SetString(PyExc_TypeError, "fast_step: 15 arguments");
+    return nullptr;
+  }
+  PyObject *td = a[12], *logits = a[13], *mask = a[14];
+  if (reinterpret_cast<PyObject*>(Py_TYPE(td)) != a[1] || !PyDict_Check(td) ||
+      PyDict_GetItem(td, key_of("action_mask")) != mask)
+    Py_RETURN_FALSE;
+  if (!PyList_Check(a[7]) || !PyList_Check(a[8])) {
+    PyErr_SetString(PyExc_TypeError, "fast_step: the action / log-probability lists");
+    return nullptr;
+  }
+  PyObject* idx = PyObject_GetAttr(a[9], a[10]);
+  if (!idx) return nullptr;
+  PyObject* zero = PyLong_FromLong(0);
+  if (!zero) {
+    Py_DECREF(idx);
+    return nullptr;
+  }
+  PyObject* args[10] = {td, logits, a[2], a[3], a[4], Py_None, zero, idx, a[5], a[6]};
+  PyObject* out = PyObject_Vectorcall(a[0], args, 10, nullptr);
+  Py_DECREF(zero);
+  if (!out || out == Py_None) {
+    Py_DECREF(idx);
+    if (!out) return nullptr;
+    Py_DECREF(out);
+    Py_RETURN_FALSE;
+  }
+  if (PyLong_Check(out)) {  // an error code: check_rc raises it
+    Py_DECREF(idx);
+    PyObject* name = PyUnicode_FromString("decode_and_step");
+    PyObject* r = nullptr;
+    if (name) {
+      PyObject* cargs[2] = {name, out};
+      r = PyObject_Vectorcall(a[11], cargs, 2, nullptr);
+      Py_DECREF(name);
+    }
+    Py_DECREF(out);
+    if (!r) return nullptr;
+    Py_DECREF(r);
+    PyErr_SetString(PyExc_RuntimeError, "decode_and_step returned a status and no outputs");
+    return nullptr;
+  }
+  if (!PyTuple_Check(out) || PyTuple_GET_SIZE(out) != 2) {
+    Py_DECREF(idx);
+    Py_DECREF(out);
+    PyErr_SetString(PyExc_TypeError, "fast_step: the step glue returned no (action, logp)");
+    return nullptr;
+  }
+  PyObject* one = PyLong_FromLong(1);
+  PyObject* nidx = one ? PyNumber_Add(idx, one) : nullptr;
+  Py_XDECREF(one);
+  Py_DECREF(idx);
+  int err = nidx ? PyObject_SetAttr(a[9], a[10], nidx) : -1;
+  Py_XDECREF(nidx);
+  if (!err) err = PyList_Append(a[7], PyTuple_GET_ITEM(out, 0));
+  if (!err) err = PyList_Append(a[8], PyTuple_GET_ITEM(out, 1));
+  Py_DECREF(out);
+  if (err) return nullptr;
+  Py_RETURN_TRUE;
+}
+
 // clear_pool() -> None: drop every pooled state storage (tensors still held stay valid)
 PyObject* clear_pool(PyObject*, PyObject* const*, Py_ssize_t) {
   g_state.clear();
@@ -1093,6 +1166,8 @@ PyMethodDef methods[] = {
     {"inplace_policy",
      reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(inplace_policy)),
      METH_FASTCALL, "(build allows in-place writes, enabled)"},
+    {"fast_step", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(fast_step)),
+     METH_FASTCALL, "the greedy decode loop's per-step closure (fast_stepper) in C"},
     {"clear_pool", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(clear_pool)),
      METH_FASTCALL, "drop the pooled step-state storages"},
     {"slab_fresh", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(slab_fresh)),

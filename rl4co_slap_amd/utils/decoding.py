@@ -22,6 +22,8 @@ from .ops import batchify, gather_by_index, unbatchify, unbatchify_and_gather
 
 _MODES = {"greedy": 0, "sampling": 1, "evaluate": 2}
 _NO_FUSED = bool(__import__("os").environ.get("CO_NO_FUSED_STEP"))  # A/B switch (tests, diag)
+# A/B switch: the greedy loop's per-step closure in Python instead of the glue's fast_step
+_NO_FAST_STEP = bool(__import__("os").environ.get("CO_NO_FAST_STEP"))
 
 # Decode math (the mode word's flag bits, include/co_env.h):
 # * "exact": ATen's CPU log_softmax restated bit for bit (SLEEF expf/logf, map_reduce_all
@@ -489,6 +491,16 @@ class DecodingStrategy(metaclass=abc.ABCMeta):
             return None
         native, mword = cached[2], cached[4]
         temp, clip, key, st = self.temperature, self.tanh_clipping, self.key, self._status
+        ts = nat.torchstep()
+        fs = ts.fast_step if ts is not None and not _NO_FAST_STEP else None
+        if fs is not None and type(self.actions) is list and type(self.logprobs) is list:
+            # the closure below in C (csrc/pycall/co_torchstep.cpp: fast_step): the same
+            # calls in the same order, without a Python frame per step
+            import functools
+
+            return functools.partial(fs, native, TensorDict, mword, temp, clip, st, key,
+                                     self.actions, self.logprobs, self, "_step_idx",
+                                     nat.check_rc)
         push_a, push_l = self.actions.append, self.logprobs.append
         dget, td_type = dict.get, TensorDict
 

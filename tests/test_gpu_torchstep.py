@@ -216,3 +216,57 @@ def test_inplace_state_writes_off_gives_same_results(dev):
     _same(on, off)
     for k in ("assignment", "action_mask", "i", "done"):
         assert torch.equal(td_on[k], td_off[k]), k
+
+
+@pytest.mark.parametrize("env_name", ["tsp", "cvrp", "slap"])
+def test_fast_step_equals_python_closure(dev, env_name, monkeypatch):
+    """The greedy loop's per-step closure in C (co_torchstep.cpp: fast_step) against the
+    Python closure it replaces (CO_NO_FAST_STEP): the same actions, rewards and
+    log-likelihoods bit for bit, and the C closure is the one bound on the GPU box."""
+    import numpy as np
+
+    from rl4co_slap_amd.envs import SLAPEnv
+    from rl4co_slap_amd.envs.slap import SLAPGenerator
+    from rl4co_slap_amd.utils import decoding as D
+
+    b = 48
+    if env_name == "slap":
+        torch.manual_seed(6)
+        np.random.seed(6)
+        data = dict(SLAPGenerator(materialize_dist_mat=False)(b).to(dev).items())
+        env_f, na = (lambda: SLAPEnv(device=dev)), 100
+    elif env_name == "tsp":
+        data = {"locs": torch.rand(b, 40, 2, generator=torch.Generator().manual_seed(7)).to(dev)}
+        env_f, na = (lambda: TSPEnv(generator_params=dict(num_loc=40), device=dev)), 40
+    else:
+        g = torch.Generator().manual_seed(8)
+        data = {"depot": torch.rand(b, 2, generator=g).to(dev),
+                "locs": torch.rand(b, 30, 2, generator=g).to(dev),
+                "demand": (((torch.rand(b, 30, generator=g) * 9).int() + 1).float() / 30.0).to(dev)}
+        env_f, na = (lambda: CVRPEnv(generator_params=dict(num_loc=30), device=dev)), 31
+    tab = torch.randn(400, b, na, generator=torch.Generator().manual_seed(12)).to(dev)
+    bound = []
+    orig = D.DecodingStrategy.fast_stepper
+
+    def spy(self, env):
+        f = orig(self, env)
+        bound.append(f)
+        return f
+
+    monkeypatch.setattr(D.DecodingStrategy, "fast_stepper", spy)
+
+    def run():
+        env = env_f()
+        td = env.reset(TensorDict({k: v.clone() for k, v in data.items()}, [b]))
+        it = iter(range(10 ** 6))
+        pol = ConstructivePolicy(None, LogitsDecoder(lambda t: tab[next(it)]), env_name=env_name,
+                                 tanh_clipping=10.0)
+        return pol(td, env, phase="test", decode_type="greedy", return_actions=True)
+
+    c = run()
+    assert bound and getattr(bound[-1], "func", None) is nat.torchstep().fast_step
+    monkeypatch.setattr(D, "_NO_FAST_STEP", True)
+    py = run()
+    assert bound[-1] is not None and getattr(bound[-1], "func", None) is None
+    _same(c, py)
+

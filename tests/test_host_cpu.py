@@ -184,3 +184,38 @@ def test_step_glue_inplace_guard():
                          cwd=ROOT, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.split()[-2:] == [str(int(expect)), "0"]
+
+
+def test_fast_step_steps_aside():
+    """fast_step returns False, having done nothing, for a td of another type or a mask
+    that is not the td's action_mask; and it checks its list arguments."""
+    ts = _native.torchstep()
+    if ts is None:
+        pytest.skip("step glue module not built")
+    fs = ts.fast_step
+    calls = []
+
+    def native(*a):
+        calls.append(a)
+        return None
+
+    class Strat:
+        _step_idx = 3
+
+    s = Strat()
+    mask = torch.ones(2, 3, dtype=torch.bool)
+    td = TensorDict({"action_mask": mask}, [2])
+    acts, lps = [], []
+    args = (native, TensorDict, 0, 1.0, 0.0, None, "action", acts, lps, s, "_step_idx",
+            _native.check_rc)
+    assert fs(*args, dict(td), None, mask) is False  # not a TensorDict
+    assert fs(*args, td, None, mask.clone()) is False  # not the td's mask
+    assert not calls
+    assert fs(*args, td, None, mask) is False  # the glue stepped aside (None)
+    assert len(calls) == 1 and calls[0][7] == 3 and s._step_idx == 3 and not acts
+    with pytest.raises(RuntimeError):  # an error code goes to check_rc
+        fs(lambda *a: 5, *args[1:], td, None, mask)
+    fs(lambda *a: ("a", "l"), *args[1:], td, None, mask)
+    assert s._step_idx == 4 and acts == ["a"] and lps == ["l"]
+    with pytest.raises(TypeError):
+        fs(*args[:7], (), lps, *args[9:], td, None, mask)
