@@ -493,6 +493,10 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
 // place from assign_in when it differs from assign, then in place; every step stores its
 // whole state as its own launch would.  The row's distances and mask units stay in
 // registers between steps; the group argmin is the single step's.
+#ifndef CO_SLAP_TCPRE
+#define CO_SLAP_TCPRE 0  // 1: products preloaded 16 steps at a time, broadcast per step (r06:
+                         // 105 -> 109 us per chunked episode at B = 65,536: off)
+#endif
 template <int KU>
 __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
     int64_t B, int L, int P, int K, const float* __restrict__ dist, const float* to_choose,
@@ -518,8 +522,16 @@ __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
   }
   int64_t it = i_a[bb];  // (every lane: one broadcast line)
   bool range = false;
+  // the products of 16 steps at a time: lane sl holds step t0 + sl's, broadcast in the
+  // group per step (ds_bpermute) -- no HBM round trip on each step's critical path
+  float tcv = 0.f;
   for (int t = 0; t < K; ++t) {
+#if CO_SLAP_TCPRE
+    if ((t & (G - 1)) == 0 && to_choose) tcv = t + sl < K ? to_choose[bb * tc_stride + t + sl] : 0.f;
+    const float prod = to_choose ? __shfl(tcv, t & (G - 1), G) : (float)(tc_stride + t);
+#else
     const float prod = to_choose ? to_choose[bb * tc_stride + t] : (float)(tc_stride + t);
+#endif
     float best = __builtin_inff();
     int bi = 0x7fffffff;
 #pragma unroll
