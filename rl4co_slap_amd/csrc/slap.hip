@@ -493,10 +493,6 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
 // place from assign_in when it differs from assign, then in place; every step stores its
 // whole state as its own launch would.  The row's distances and mask units stay in
 // registers between steps; the group argmin is the single step's.
-#ifndef CO_SLAP_TCPRE
-#define CO_SLAP_TCPRE 0  // 1: products preloaded 16 steps at a time, broadcast per step (r06:
-                         // 105 -> 109 us per chunked episode at B = 65,536: off)
-#endif
 template <int KU>
 __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
     int64_t B, int L, int P, int K, const float* __restrict__ dist, const float* to_choose,
@@ -522,16 +518,20 @@ __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
   }
   int64_t it = i_a[bb];  // (every lane: one broadcast line)
   bool range = false;
-  // the products of 16 steps at a time: lane sl holds step t0 + sl's, broadcast in the
-  // group per step (ds_bpermute) -- no HBM round trip on each step's critical path
-  float tcv = 0.f;
-  for (int t = 0; t < K; ++t) {
-#if CO_SLAP_TCPRE
-    if ((t & (G - 1)) == 0 && to_choose) tcv = t + sl < K ? to_choose[bb * tc_stride + t + sl] : 0.f;
-    const float prod = to_choose ? __shfl(tcv, t & (G - 1), G) : (float)(tc_stride + t);
-#else
-    const float prod = to_choose ? to_choose[bb * tc_stride + t] : (float)(tc_stride + t);
-#endif
+  // per-row pointers formed once (the lane's first mask unit, the row's scalars, the
+  // action column advanced by the row stride each step): the step itself does no 64-bit
+  // address arithmetic but the product's assignment entry
+  uint32_t* const mo_a = reinterpret_cast<uint32_t*>(mask_a + b * (int64_t)L) + sl;
+  uint32_t* const mo_b = reinterpret_cast<uint32_t*>(mask_b + b * (int64_t)L) + sl;
+  int64_t* const ip_a = i_a + b;
+  int64_t* const ip_b = i_b + b;
+  int64_t* ap = action_out + b;
+  int32_t* const arow = assign + b * P;
+  const int32_t* const arow_in = assign_in + b * P;
+  const float* tcp = to_choose ? to_choose + bb * tc_stride : nullptr;
+  // one step: reads the mask units in registers, writes mask row `mo` and i `ip`
+  auto step = [&](int t, uint32_t* mo, int64_t* ip) {
+    const float prod = tcp ? tcp[t] : (float)(tc_stride + t);
     float best = __builtin_inff();
     int bi = 0x7fffffff;
 #pragma unroll
@@ -551,7 +551,6 @@ __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
       }
     }
     grp_argmin_split<G>(best, bi);
-    const bool to_b = (t & 1) == 0;
 #pragma unroll
     for (int k = 0; k < KU; ++k) {
       const int u = sl + G * k;
@@ -559,30 +558,34 @@ __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
       mv[k] &= clr;
     }
     if (live) {
-      int64_t p = (int64_t)(int)prod;  // .to(torch.int), slap/env.py:52
+      int p = (int)prod;  // .to(torch.int), slap/env.py:52
       if (p < 0) p += P;
       const bool p_ok = p >= 0 && p < P;
       if (t == 0 && assign_in != assign)  // out of place: the row with [p] = action
-        for (int c = sl; c < P; c += G) assign[b * P + c] = c == p ? (int32_t)bi : assign_in[b * P + c];
-      uint32_t* mo = reinterpret_cast<uint32_t*>((to_b ? mask_b : mask_a) + b * (int64_t)L);
+        for (int c = sl; c < P; c += G) arow[c] = c == p ? (int32_t)bi : arow_in[c];
 #pragma unroll
-      for (int k = 0; k < KU; ++k) {
-        const int u = sl + G * k;
-        if (u < U) mo[u] = mv[k];
-      }
+      for (int k = 0; k < KU; ++k)
+        if (sl + G * k < U) mo[G * k] = mv[k];
       if (sl == 0) {
-        action_out[(int64_t)t * astride + b] = bi;
+        *ap = bi;
         if (!p_ok)
           range = true;
         else if (t > 0 || assign_in == assign)
-          assign[b * P + p] = (int32_t)bi;
+          arow[p] = (int32_t)bi;
         done[b] = it == (int64_t)(P - 1);
-        (to_b ? i_b : i_a)[b] = it + 1;
+        *ip = it + 1;
         reward[b] = 0;
       }
     }
+    ap += astride;
     it += 1;
+  };
+  int t = 0;
+  for (; t + 1 < K; t += 2) {  // step t reads A and writes B, step t + 1 the reverse
+    step(t, mo_b, ip_b);
+    step(t + 1, mo_a, ip_a);
   }
+  if (t < K) step(t, mo_b, ip_b);
   if (range) set_status(status, CO_ST_INDEX_RANGE);
 }
 

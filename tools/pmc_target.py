@@ -105,12 +105,14 @@ else:
     b = 65536 if args.kernel.endswith("b65536") else 16384
     td = SLAPGenerator(materialize_dist_mat=False)(b).to(dev)
     if args.kernel.startswith("slap_stepwise"):  # slap_stepwise_{closest,teacher}[_b65536]
-        pol = "closest" if "closest" in args.kernel else "teacher"
+        pol = "closest" if ("closest" in args.kernel or "chunked" in args.kernel) else "teacher"
         acts = None
         if pol == "teacher":
             torch.manual_seed(4321)
             acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
-        ep = engine.SLAPStepwiseEpisode(td, acts, policy=pol)
+        # slap_stepwise_chunked_b65536: the closest policy, 10 steps per co_slap_closest_steps
+        ep = engine.SLAPStepwiseEpisode(td, acts, policy=pol,
+                                        chunk=10 if "chunked" in args.kernel else 1)
     elif args.kernel.startswith("slap_fused_random"):
         torch.manual_seed(4321)
         acts = (torch.rand(b, 99).argsort(1)[:, :20] + 1).to(dev)
