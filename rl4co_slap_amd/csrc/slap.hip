@@ -493,6 +493,37 @@ __global__ __launch_bounds__(256) void slap_closest_step_kernel(
 // place from assign_in when it differs from assign, then in place; every step stores its
 // whole state as its own launch would.  The row's distances and mask units stay in
 // registers between steps; the group argmin is the single step's.
+#ifndef CO_SLAP_SSORT
+#define CO_SLAP_SSORT 1  // the steps kernel pops per-lane sorted candidate keys (0: masked scan)
+#endif
+// per-lane ascending sort of u64 keys (Batcher odd-even merge; one v_cmp_lt_u64 and four
+// selects per comparator), the candidate order of the closest-free steps
+__device__ __forceinline__ uint32_t key_sel32(uint64_t m, uint32_t t, uint32_t f) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+__device__ __forceinline__ void key_cswap(uint64_t& a, uint64_t& b) {
+  const uint64_t lt = __builtin_amdgcn_ballot_w64(a < b);
+  const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b,
+                 bhi = (uint32_t)(b >> 32);
+  a = ((uint64_t)key_sel32(lt, ahi, bhi) << 32) | key_sel32(lt, alo, blo);
+  b = ((uint64_t)key_sel32(lt, bhi, ahi) << 32) | key_sel32(lt, blo, alo);
+}
+template <int E>
+__device__ __forceinline__ void sort_keys_asc(uint64_t (&k)[E]) {
+  static_assert((E & (E - 1)) == 0, "E must be a power of two");
+#pragma unroll
+  for (int p = 1; p < E; p <<= 1)
+#pragma unroll
+    for (int q = p; q > 0; q >>= 1)
+#pragma unroll
+      for (int j = q % p; j + q < E; j += 2 * q)
+#pragma unroll
+        for (int i = 0; i < q; ++i)
+          if (i + j + q < E && (i + j) / (2 * p) == (i + j + q) / (2 * p)) key_cswap(k[i + j], k[i + j + q]);
+}
+
 template <int KU>
 __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
     int64_t B, int L, int P, int K, const float* __restrict__ dist, const float* to_choose,
@@ -529,9 +560,57 @@ __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
   int32_t* const arow = assign + b * P;
   const int32_t* const arow_in = assign_in + b * P;
   const float* tcp = to_choose ? to_choose + bb * tc_stride : nullptr;
+#if CO_SLAP_SSORT
+  // closest-free = the free locations in increasing (distance, index) order: each lane
+  // sorts its candidates once per launch (key: order-preserving u32 of the distance, +inf
+  // for a taken location, then the index); a step is a group min over the lanes' heads and
+  // a pop by the owner (the head and next key in registers, the rest in LDS) instead of a
+  // masked scan of every candidate.  A key not below +inf's is never chosen; with none left
+  // the action is 0 and byte 0 is cleared, as the scan's argmin of all-inf does.
+  constexpr int EPL = KU == 3 ? 16 : 4 * KU;
+  constexpr uint32_t kOrdInf = 0xff800000u;  // ordered key of +inf
+  __shared__ uint64_t s_keys[(EPL - 2) * 256];
+  uint64_t hk, nk;
+  int h = 2;
+  {
+    uint64_t key[EPL];
+#pragma unroll
+    for (int k = 0; k < EPL / 4; ++k) {
+      const int u = sl + G * k;
+      const float d4[4] = {dv[k < KU ? k : 0].x, dv[k < KU ? k : 0].y, dv[k < KU ? k : 0].z,
+                           dv[k < KU ? k : 0].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool ok = k < KU && u < U && ((mv[k < KU ? k : 0] >> (8 * j)) & 0xffu);
+        // -0.0 keyed as +0.0 (d + 0.0): they tie as in argmin's float compare
+        const uint32_t uu = __float_as_uint(ok ? d4[j] + 0.0f : __builtin_inff());
+        const uint32_t ord = uu ^ ((uint32_t)((int32_t)uu >> 31) | 0x80000000u);
+        key[4 * k + j] = (k < KU && u < U) ? (((uint64_t)ord << 32) | (uint32_t)(4 * u + j)) : ~0ull;
+      }
+    }
+    sort_keys_asc<EPL>(key);
+    hk = key[0];
+    nk = key[1];
+#pragma unroll
+    for (int k = 2; k < EPL; ++k) s_keys[(k - 2) * 256 + threadIdx.x] = key[k];
+  }
+#endif
   // one step: reads the mask units in registers, writes mask row `mo` and i `ip`
   auto step = [&](int t, uint32_t* mo, int64_t* ip) {
     const float prod = tcp ? tcp[t] : (float)(tc_stride + t);
+#if CO_SLAP_SSORT
+    const uint32_t hh = (uint32_t)(hk >> 32);
+    const uint32_t gm = grp_reduce<G>(hh, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+    const uint32_t cand = hh == gm ? (uint32_t)hk : 0xffffffffu;
+    const uint32_t gi = grp_reduce<G>(cand, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
+    const bool any = gm < kOrdInf;
+    const int bi = any ? (int)gi : 0;
+    if (any && (uint32_t)hk == gi) {  // the owner's head is the chosen location: pop it
+      hk = nk;
+      nk = h < EPL ? s_keys[(h - 2) * 256 + threadIdx.x] : ~0ull;
+      ++h;
+    }
+#else
     float best = __builtin_inff();
     int bi = 0x7fffffff;
 #pragma unroll
@@ -551,6 +630,7 @@ __global__ __launch_bounds__(256) void slap_closest_steps_kernel(
       }
     }
     grp_argmin_split<G>(best, bi);
+#endif
 #pragma unroll
     for (int k = 0; k < KU; ++k) {
       const int u = sl + G * k;
