@@ -68,6 +68,17 @@ def main():
         out = bench.bench_dropin_cvrp(32768, 100, a.k, 1, 0, dev)
     elif a.mode == "dropin_slap":
         out = bench.bench_dropin_slap(16384, a.k, 1, 0, dev)
+    elif a.mode == "tsp_chunks":  # teacher-forced stepwise TSP-100 at B = 65,536, chunk sweep
+        from rl4co_slap_amd.rollout.engine import TSPStepwiseEpisode
+
+        locs, acts = bench.tsp_inputs(65536, 100, 0)
+        locs, acts = locs.to(dev), acts.to(dev)
+        out = {}
+        for c in (1, 10, 25):
+            ep = TSPStepwiseEpisode(locs, acts, chunk=c).capture()
+            wall, ev = bench.timed(ep.replay, a.k, 2, 1, dev)
+            out[c] = {"us_per_episode": round(wall / a.k * 1e6, 2)}
+            del ep
     elif a.mode == "slap_chunks":  # closest-free stepwise SLAP at B = 65,536, chunk sweep
         from rl4co_slap_amd.envs.slap import SLAPGenerator
         from rl4co_slap_amd.rollout.engine import SLAPStepwiseEpisode
